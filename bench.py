@@ -1,0 +1,266 @@
+"""Benchmark: quantized-conv forward images/s, ResNet56 224x224, bs=256 per GPU.
+
+One step = one pass of the hot path over one batch: the 56 QuantizedConv2d
+layers of ResNet56 in graph order (each a fused PO2 quantize + conv, i.e. the
+reference's QuantizedConv2d.forward, models/quantized_conv.py:32-38), fed by
+the previous layer's output, then the classifier head (global avg-pool + fc)
+and, for N > 1, an RCCL all_gather of the logits over xGMI.  Inputs and
+weights are synthetic (seeded) and resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from po2_quantization_amd import _lib  # noqa: E402
+
+METRIC = "quantized-conv fwd images/sec, ResNet56 224×224 bs=256; 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, FP32 matrix (= vector) peak
+PEAK_BF16_MFMA_TFLOPS = 2516.6     # dense bf16
+PEAK_HBM_GBS = 8000.0              # HBM3E spec
+
+
+def resnet_qconv_layers(n_blocks):
+    """(name, C, K, R, stride, pad, role) of every QuantizedConv2d, graph order
+    (reference models/resnet.py:25-50, 150-163): role in {conv1, conv2, ds}."""
+    layers, inplanes = [], 16
+    for stage, (planes, stride) in enumerate(((16, 1), (32, 2), (64, 2))):
+        for b in range(n_blocks):
+            st = stride if b == 0 else 1
+            pre = "layer%d.%d" % (stage + 1, b)
+            layers.append((pre + ".conv1", inplanes, planes, 3, st, 1, "conv1"))
+            layers.append((pre + ".conv2", planes, planes, 3, 1, 1, "conv2"))
+            if st != 1 or inplanes != planes:
+                layers.append((pre + ".downsample.0", inplanes, planes, 1, st, 0, "ds"))
+            inplanes = planes
+    return layers
+
+
+def kaiming(K, C, R, gen, dev):
+    return (torch.randn(K, C, R, R, generator=gen) * math.sqrt(2.0 / (K * R * R))).to(dev)
+
+
+class QConvChain:
+    def __init__(self, n_blocks, num_classes, mode, bits, precision, dev, seed=0):
+        g = torch.Generator().manual_seed(seed)
+        self.layers = resnet_qconv_layers(n_blocks)
+        self.weights = [kaiming(K, C, R, g, dev) for (_, C, K, R, _, _, _) in self.layers]
+        self.fc_w = (torch.randn(num_classes, 64, generator=g) * 0.05).to(dev)
+        self.fc_b = torch.zeros(num_classes, device=dev)
+        self.mode, self.bits, self.precision = mode, bits, precision
+        self.timed_layer = None      # index of the layer whose launches are timed
+        self.events = []
+
+    def conv(self, i, x):
+        _, C, K, R, st, pad, _ = self.layers[i]
+        return _lib.qconv2d(x, self.weights[i], None, st, pad, 1, 1, self.bits, self.mode, 1, self.precision)
+
+    def forward(self, x, record=False):
+        i = 0
+        while i < len(self.layers):
+            name, _, _, _, _, _, role = self.layers[i]
+            assert role == "conv1"
+            has_ds = i + 2 < len(self.layers) and self.layers[i + 2][6] == "ds"
+            out = self._timed(i, x, record)
+            out = self._timed(i + 1, out, record)
+            if has_ds:
+                self._timed(i + 2, x, record)  # projection shortcut (its output feeds the add)
+                i += 3
+            else:
+                i += 2
+            x = out
+        pooled = x.mean(dim=(2, 3))
+        return torch.nn.functional.linear(pooled, self.fc_w, self.fc_b)
+
+    def _timed(self, i, x, record):
+        if record and self.layers[i][1:3] == self.layers[self.timed_layer][1:3] and \
+                self.layers[i][3:6] == self.layers[self.timed_layer][3:6]:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            y = self.conv(i, x)
+            e1.record()
+            self.events.append((e0, e1))
+            return y
+        return self.conv(i, x)
+
+
+def conv_work(N, C, H, K, R, st, pad):
+    P = (H + 2 * pad - R) // st + 1
+    flops = 2.0 * N * K * P * P * C * R * R
+    # fp32 in + out + weight read twice (absmax pass + conv) — BASELINE.md roofline table
+    nbytes = 4.0 * (N * C * H * H + N * K * P * P + 2 * K * C * R * R)
+    return flops, nbytes
+
+
+def cpu_baseline(layers, weights_cpu, image, mode, bits, seconds):
+    """The reference's CPU path restated (oracle quantizer + torch CPU F.conv2d, the
+    same oneDNN conv the reference calls) over a bounded sample of the workload."""
+    from oracle import oracle as O
+
+    threads = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        threads = min(threads, int(omp))
+    torch.set_num_threads(threads)
+    nb = 2
+    g = torch.Generator().manual_seed(1)
+    x0 = torch.relu(torch.randn(nb, 16, image, image, generator=g))
+
+    def one_pass():
+        x = x0
+        i = 0
+        while i < len(layers):
+            has_ds = i + 2 < len(layers) and layers[i + 2][6] == "ds"
+            outs = []
+            for j in range(i, i + (3 if has_ds else 2)):
+                _, C, K, R, st, pad, role = layers[j]
+                inp = x if role != "conv2" else outs[-1]
+                outs.append(O.cpu_reference_qconv2d(inp, weights_cpu[j], None, st, pad, 1, 1, bits, mode))
+            x = outs[1]
+            i += 3 if has_ds else 2
+        return x
+
+    one_pass()  # warm-up (oneDNN primitive creation)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        one_pass()
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(nb * reps / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "%d passes x %d images of the ResNet56 %dx%d quantized-conv chain (oracle quantizer "
+                      "+ torch CPU F.conv2d/oneDNN, %d threads), %.1f s" % (reps, nb, image, image, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--model", default="resnet56", choices=["resnet20", "resnet32", "resnet44", "resnet56"])
+    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--quantizer", default="po2", choices=["po2", "po2+", "none"])
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--precision", default="auto", choices=["auto", "fp32", "bf16x3"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    n_blocks = {"resnet20": 3, "resnet32": 5, "resnet44": 7, "resnet56": 9}[args.model]
+    chain = QConvChain(n_blocks, args.classes, args.quantizer, args.bits, args.precision, dev, seed=0)
+    chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
+    B, Hs = args.batch, args.image
+    x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
+    gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
+
+    def step(record=False):
+        logits = chain.forward(x, record)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, logits)
+        return logits
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(record=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+
+    # dominant op: fused quantize+conv of the timed shape, HIP events on its stream
+    ev_ms = [a.elapsed_time(b) for a, b in chain.events]
+    avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
+    _, C, K, R, st, pad, _ = chain.layers[chain.timed_layer]
+    flops, nbytes = conv_work(B, C, Hs, K, R, st, pad)
+    prec = "fp32" if args.precision == "auto" else args.precision
+    if prec == "bf16x3":
+        peak_c = PEAK_BF16_MFMA_TFLOPS / 3.0
+    else:
+        peak_c = PEAK_FP32_MFMA_TFLOPS
+    hbm_bound = flops / nbytes * PEAK_HBM_GBS / 1e3 < peak_c  # TFLOP/s attainable from HBM
+    if hbm_bound:
+        achieved = nbytes / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4)}
+    else:
+        achieved = flops / (avg_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak_c, 1), "unit": "TFLOP/s",
+                "frac": round(achieved / peak_c, 4)}
+    roof["traffic"] = None
+    traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file)).get("%s/%s/%d" % (prec, args.model, Hs))
+            roof["traffic"] = tr
+        except (ValueError, OSError):
+            pass
+    roof.update({"kernel": "fused po2 quantize+conv 3x3 %d->%d @%dx%d bs=%d (absmax+pack+conv launches)"
+                           % (C, K, Hs, Hs, B),
+                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(nbytes), "flops": int(flops)})
+
+    images = world * B * args.steps
+    out = {
+        "metric": METRIC, "value": round(images / dt, 2), "unit": "images/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3-split MFMA)", "data": "synthetic",
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s"
+                               % (args.model, len(chain.layers), args.quantizer, args.bits,
+                                  " + RCCL all_gather(logits)" if world > 1 else ""),
+                   "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
+                   "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        wcpu = [w.cpu() for w in chain.weights]
+        out["cpu_baseline"] = cpu_baseline(chain.layers, wcpu, Hs, args.quantizer, args.bits, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,85 @@
+/*
+ * po2q — MI355X (gfx950) power-of-two quantized convolution, C ABI.
+ *
+ * The drop-in boundary for the reference's hot path (mschoenb97/po2_quantization):
+ * plain pointers, sizes and a HIP stream handle; no torch types.  Every entry
+ * point is asynchronous on `stream` (no host synchronisation, no allocation):
+ * the caller owns every buffer, including the workspace whose size the
+ * matching *_workspace_bytes() function returns.  All device pointers are
+ * device-resident fp32, contiguous NCHW / [K, C/groups, R, S].
+ *
+ * Return value: PO2Q_OK (0) or a PO2Q_ERR_* code; po2q_last_error() then
+ * holds a message (thread-local).  Invalid arguments are rejected before any
+ * launch, so an error leaves every output untouched.
+ */
+#ifndef PO2Q_H_
+#define PO2Q_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* quantizer selection — the reference's quantizer_dict keys (utils/quantizers.py:156-161)
+ * plus "no quantizer" (QuantizedConv2d with quantize_fn=None, quantized_conv.py:37-38) */
+enum po2q_mode { PO2Q_MODE_NONE = 0, PO2Q_MODE_PO2 = 1, PO2Q_MODE_PO2_PLUS = 2 };
+
+/* conv arithmetic (flags of po2q_qconv2d_f32) */
+enum po2q_precision {
+    PO2Q_PREC_AUTO = 0,   /* library default (currently PO2Q_PREC_FP32) */
+    PO2Q_PREC_FP32 = 1,   /* fp32-input MFMA, exact fp32 fma chain */
+    PO2Q_PREC_BF16X3 = 2  /* bf16 MFMA, activations split hi+mid+lo (exact), weights 2^e (exact) */
+};
+
+enum po2q_status {
+    PO2Q_OK = 0,
+    PO2Q_ERR_INVALID = 1,     /* bad shape / argument (reference: RuntimeError from torch) */
+    PO2Q_ERR_UNSUPPORTED = 2, /* valid for the reference but not implemented here */
+    PO2Q_ERR_WORKSPACE = 3,   /* workspace too small */
+    PO2Q_ERR_HIP = 4          /* HIP runtime error at launch */
+};
+
+const char* po2q_version(void);
+const char* po2q_last_error(void);
+
+/*
+ * PO2 / PO2+ weight quantizer.
+ * Replaces PowerOfTwoQuantizer.forward      (utils/quantizers.py:19-32)
+ *      and PowerOfTwoPlusQuantizer.forward  (utils/quantizers.py:39-52)
+ * out[i] = 2^e_i * sign(w_i) * max|w|, e_i = clamp(round(log2|w_i/max|w||), fsr-2^(bits-1), fsr-1)
+ * (po2+: round(log2(a/1.5)+0.5)), bit-exact with the reference incl. NaN/inf/±0.
+ * n == 0 is rejected (the reference's torch.max raises on an empty tensor).
+ * mode: PO2Q_MODE_PO2 or PO2Q_MODE_PO2_PLUS.  1 <= bits <= 16.
+ */
+size_t po2q_quantize_workspace_bytes(int64_t n);
+int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, int mode,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Quantized 2-D convolution forward (quantize weight, then conv; NCHW fp32).
+ * Replaces QuantizedConv2d.forward (models/quantized_conv.py:32-38), i.e.
+ * F.conv2d(x, quantize_fn.apply(weight, bits), bias, stride, padding, dilation, groups);
+ * mode PO2Q_MODE_NONE is the plain conv of quantize_fn=None (:37-38).
+ * x [N, C, H, W], w [K, C/groups, R, S], bias [K] or NULL, y [N, K, P, Q] with
+ * P = (H + 2*pad_h - dil_h*(R-1) - 1)/stride_h + 1 (likewise Q).
+ * flags: one of enum po2q_precision.
+ */
+size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W,
+                                    int64_t K, int64_t R, int64_t S,
+                                    int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                                    int64_t dil_h, int64_t dil_w, int64_t groups, int mode, int flags);
+int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y,
+                     int64_t N, int64_t C, int64_t H, int64_t W,
+                     int64_t K, int64_t R, int64_t S,
+                     int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                     int64_t dil_h, int64_t dil_w, int64_t groups,
+                     int bits, int fsr, int mode, int flags,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PO2Q_H_ */

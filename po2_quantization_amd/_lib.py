@@ -1,0 +1,146 @@
+"""ctypes binding of the po2q C ABI (include/po2q.h) for torch tensors.
+
+This is the only bridge between Python and the HIP kernels.  Tensors are handed
+over as raw device pointers plus sizes, and launches go onto torch's current
+HIP stream, so the ops compose with torch streams and graph capture.  There is
+deliberately no CPU or torch fallback: a missing library or a non-HIP / non-fp32
+tensor raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PO2Q_LIB", os.path.join(_HERE, "lib", "libpo2q.so"))
+
+MODES = {None: 0, "none": 0, "po2": 1, "po2+": 2}
+PRECISIONS = {"auto": 0, "fp32": 1, "bf16x3": 2}
+
+# every symbol include/po2q.h declares (checked by tests/test_capi.py)
+EXPORTS = (
+    "po2q_version",
+    "po2q_last_error",
+    "po2q_quantize_workspace_bytes",
+    "po2q_quantize_f32",
+    "po2q_qconv2d_workspace_bytes",
+    "po2q_qconv2d_f32",
+)
+
+_lib = None
+
+
+class Po2qError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libpo2q.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise Po2qError(
+            "po2q: native library %s not found; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C po2_quantization_amd/csrc`" % LIB_PATH
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    i64, i32, p, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    L.po2q_version.restype = ctypes.c_char_p
+    L.po2q_version.argtypes = []
+    L.po2q_last_error.restype = ctypes.c_char_p
+    L.po2q_last_error.argtypes = []
+    L.po2q_quantize_workspace_bytes.restype = sz
+    L.po2q_quantize_workspace_bytes.argtypes = [i64]
+    L.po2q_quantize_f32.restype = i32
+    L.po2q_quantize_f32.argtypes = [p, p, i64, i32, i32, i32, p, sz, p]
+    L.po2q_qconv2d_workspace_bytes.restype = sz
+    L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32]
+    L.po2q_qconv2d_f32.restype = i32
+    L.po2q_qconv2d_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+    _lib = L
+    return L
+
+
+def _check(status):
+    if status != 0:
+        raise Po2qError(load().po2q_last_error().decode())
+
+
+def _require_hip_f32(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("po2q: %s must be a torch.Tensor" % what)
+    if t.device.type != "cuda":
+        raise Po2qError("po2q: %s must be a HIP device tensor (got %s); the po2q ops have no CPU path"
+                        % (what, t.device))
+    if t.dtype != torch.float32:
+        raise Po2qError("po2q: %s must be float32 (got %s)" % (what, t.dtype))
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _workspace(nbytes, dev):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+
+
+def quantize(w, bits, mode, fsr=1):
+    """PO2 / PO2+ quantization of a whole tensor (utils/quantizers.py:19-56)."""
+    _require_hip_f32(w, "input")
+    L = load()
+    mode_id = MODES[mode]
+    if mode_id == 0:
+        raise Po2qError("po2q: quantize() needs mode 'po2' or 'po2+'")
+    wc = w.contiguous()
+    out = torch.empty_like(wc)
+    n = wc.numel()
+    with torch.cuda.device(wc.device):
+        ws = _workspace(L.po2q_quantize_workspace_bytes(n), wc.device)
+        _check(L.po2q_quantize_f32(wc.data_ptr(), out.data_ptr(), n, int(bits), int(fsr), mode_id,
+                                   ws.data_ptr(), ws.numel(), _stream(wc.device)))
+    return out
+
+
+def _pair(v):
+    return (int(v), int(v)) if isinstance(v, int) else (int(v[0]), int(v[1]))
+
+
+def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+            precision="auto"):
+    """Fused quantize + conv forward (models/quantized_conv.py:32-38); NCHW fp32 in/out."""
+    _require_hip_f32(x, "input")
+    _require_hip_f32(w, "weight")
+    if bias is not None:
+        _require_hip_f32(bias, "bias")
+    if x.dim() != 4 or w.dim() != 4:
+        raise Po2qError("po2q: expected 4-D input and weight, got %d-D and %d-D" % (x.dim(), w.dim()))
+    if x.device != w.device or (bias is not None and bias.device != x.device):
+        raise Po2qError("po2q: input, weight and bias must be on the same device")
+    L = load()
+    N, C, H, W = x.shape
+    K, Cg, R, S = w.shape
+    if Cg * groups != C:
+        raise Po2qError("po2q: Given groups=%d, weight of size %s, expected input%s to have %d channels, but got "
+                        "%d channels instead" % (groups, list(w.shape), list(x.shape), Cg * groups, C))
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    dh, dw = _pair(dilation)
+    P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+    Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+    args = (N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, int(groups))
+    mode_id = MODES[mode]
+    prec = PRECISIONS[precision]
+    xc = x.contiguous()
+    wc = w.contiguous()
+    bc = bias.contiguous() if bias is not None else None
+    with torch.cuda.device(xc.device):
+        nbytes = L.po2q_qconv2d_workspace_bytes(*args, mode_id, prec)
+        if nbytes == 0:
+            _check(1)
+        y = torch.empty((N, K, max(P, 0), max(Q, 0)), dtype=torch.float32, device=xc.device)
+        ws = _workspace(nbytes, xc.device)
+        _check(L.po2q_qconv2d_f32(xc.data_ptr(), wc.data_ptr(), bc.data_ptr() if bc is not None else None,
+                                  y.data_ptr(), *args, int(bits), int(fsr), mode_id, prec,
+                                  ws.data_ptr(), ws.numel(), _stream(xc.device)))
+    return y

@@ -1,0 +1,125 @@
+// C ABI of the po2q library (include/po2q.h): argument validation, workspace
+// layout and dispatch.  Everything is enqueued on the caller's stream; nothing
+// here allocates device memory or synchronises.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "../../include/po2q.h"
+#include "po2q_internal.h"
+
+namespace po2q {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace po2q
+
+using namespace po2q;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+bool check_mode_bits(int mode, int bits, bool allow_none) {
+    if (mode != PO2Q_MODE_PO2 && mode != PO2Q_MODE_PO2_PLUS && !(allow_none && mode == PO2Q_MODE_NONE)) {
+        set_error("po2q: unknown quantizer mode " + std::to_string(mode));
+        return false;
+    }
+    if (mode != PO2Q_MODE_NONE && (bits < 1 || bits > 16)) {
+        set_error("po2q: bits must be in [1, 16], got " + std::to_string(bits));
+        return false;
+    }
+    return true;
+}
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return PO2Q_OK;
+    set_error(std::string("po2q: ") + what + ": " + hipGetErrorString(e));
+    return PO2Q_ERR_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* po2q_version(void) { return "po2q 0.1.0 (gfx950)"; }
+
+const char* po2q_last_error(void) { return g_last_error.c_str(); }
+
+size_t po2q_quantize_workspace_bytes(int64_t n) {
+    if (n <= 0) return 0;
+    return align_up((size_t)absmax_blocks(n) * sizeof(unsigned));
+}
+
+int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, int mode, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+    if (n <= 0) {
+        set_error("po2q: max(): Expected reduction dim to be specified for input.numel() == 0");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!check_mode_bits(mode, bits, false)) return PO2Q_ERR_INVALID;
+    if (!w || !out || !workspace) {
+        set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (workspace_bytes < po2q_quantize_workspace_bytes(n)) {
+        set_error("po2q: quantize workspace too small");
+        return PO2Q_ERR_WORKSPACE;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    unsigned* partial = reinterpret_cast<unsigned*>(workspace);
+    const int nb = absmax_blocks(n);
+    int st = hip_status(launch_absmax(w, n, partial, nb, s), "absmax launch");
+    if (st) return st;
+    return hip_status(launch_quantize_plain(w, n, partial, nb, bits, fsr, mode, out, s), "quantize launch");
+}
+
+size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                                    int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h,
+                                    int64_t dil_w, int64_t groups, int mode, int flags) {
+    ConvPlan p;
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, flags))
+        return 0;
+    const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
+    return align_up((size_t)absmax_blocks(nw) * sizeof(unsigned)) + align_up((size_t)p.packed_floats * sizeof(float));
+}
+
+int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
+                     int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
+                     int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode,
+                     int flags, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!check_mode_bits(mode, bits, true)) return PO2Q_ERR_INVALID;
+    if (flags < PO2Q_PREC_AUTO || flags > PO2Q_PREC_BF16X3) {
+        set_error("po2q: unknown precision flag " + std::to_string(flags));
+        return PO2Q_ERR_INVALID;
+    }
+    if (!x || !w || !y || !workspace) {
+        set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    ConvPlan p;
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
+    const size_t part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
+    const size_t need = part_bytes + align_up((size_t)p.packed_floats * sizeof(float));
+    if (workspace_bytes < need) {
+        set_error("po2q: conv workspace too small (need " + std::to_string(need) + " bytes)");
+        return PO2Q_ERR_WORKSPACE;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    unsigned* partial = reinterpret_cast<unsigned*>(workspace);
+    float* packed = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part_bytes);
+    const int nb = absmax_blocks(nw);
+    int st;
+    if (mode != PO2Q_MODE_NONE) {
+        st = hip_status(launch_absmax(w, nw, partial, nb, s), "absmax launch");
+        if (st) return st;
+    }
+    st = hip_status(launch_pack_weights(p, w, partial, nb, bits, fsr, mode, packed, s), "weight pack launch");
+    if (st) return st;
+    return hip_status(launch_conv(p, x, packed, bias, y, s), "conv launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,318 @@
+// Convolution kernels for gfx950 (QuantizedConv2d.forward, models/quantized_conv.py:32-38,
+// i.e. F.conv2d(x, Q(w), bias, stride, padding, dilation, groups), NCHW fp32).
+//
+// kind 0  conv_mfma_f32: LDS-staged implicit GEMM on v_mfma_f32_16x16x4_f32.
+//         D[out-channel][pixel] += W[out-channel][c..c+3 @ tap] * X[c..c+3 @ tap][pixel]
+//         Block = 4 waves; tile = 16*MI output channels x TP*TQ output pixels of
+//         one image; each wave owns NJ groups of 16 pixels.  Per input-channel
+//         chunk the halo tile [CC][HH][WW] (fp32, NCHW order, zero padded) and
+//         the chunk's packed weights are staged in LDS; fragments are read with
+//         conflict-free ds_read_b32 (pixels on lanes, channels on lane>>4).
+// kind 1  conv_depthwise: direct conv, one output pixel per lane (HBM-bound).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+
+#include "po2q_internal.h"
+
+namespace po2q {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct ConvArgs {
+    int N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups;
+    int P, Q, Cg, Kg;
+    int TP, TQ, tilesP, tilesQ, CC, nchunks, kblocks;
+    int HH, WW, WWp, PS, steps;
+};
+
+static ConvArgs to_args(const ConvPlan& p) {
+    ConvArgs a;
+    a.N = p.N; a.C = p.C; a.H = p.H; a.W = p.W; a.K = p.K; a.R = p.R; a.S = p.S;
+    a.sh = p.sh; a.sw = p.sw; a.ph = p.ph; a.pw = p.pw; a.dh = p.dh; a.dw = p.dw; a.groups = p.groups;
+    a.P = p.P; a.Q = p.Q; a.Cg = p.Cg; a.Kg = p.Kg;
+    a.TP = p.TP; a.TQ = p.TQ; a.tilesP = p.tilesP; a.tilesQ = p.tilesQ; a.CC = p.CC;
+    a.nchunks = p.nchunks; a.kblocks = p.kblocks;
+    a.HH = p.HH; a.WW = p.WW; a.WWp = p.WWp; a.PS = p.PS; a.steps = p.steps;
+    return a;
+}
+
+template <int MI, int NJ>
+__global__ __launch_bounds__(kThreads) void conv_mfma_f32(const float* __restrict__ x,
+                                                          const float* __restrict__ wpk,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ y, ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* xs = smem;                  // [CC][PS]  halo tile, plane stride PS, row stride WWp
+    float* wsm = smem + a.CC * a.PS;   // [steps][MI][64] packed weights of the chunk
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int bid = blockIdx.x;
+    const int tiles = a.tilesP * a.tilesQ;
+    const int tile = bid % tiles; bid /= tiles;
+    const int kb = bid % a.kblocks; bid /= a.kblocks;
+    const int g = bid % a.groups;
+    const int n = bid / a.groups;
+    const int p0 = (tile / a.tilesQ) * a.TP, q0 = (tile % a.tilesQ) * a.TQ;
+    const int h0 = p0 * a.sh - a.ph, w0 = q0 * a.sw - a.pw;
+    const int npix = a.TP * a.TQ;
+
+    int poff[NJ];
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+        int slot = (wave * NJ + nj) * 16 + (lane & 15);
+        if (slot >= npix) slot = 0;
+        const int pl = slot / a.TQ, ql = slot - pl * a.TQ;
+        poff[nj] = pl * a.sh * a.WWp + ql * a.sw + (lane >> 4) * a.PS;
+    }
+
+    floatx4 acc[MI][NJ];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < NJ; ++nj) acc[mi][nj] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int chunk_floats = a.steps * MI * 64;
+    const float* wsrc = wpk + (int64_t)(g * a.kblocks + kb) * a.nchunks * chunk_floats;
+    const int c4n = a.CC >> 2;
+
+    for (int chunk = 0; chunk < a.nchunks; ++chunk) {
+        const int c0 = chunk * a.CC;
+        // ---- stage halo tile: one (channel, row) per wave iteration, lanes along W
+        const float* xg = x + ((int64_t)n * a.C + (int64_t)g * a.Cg + c0) * a.H * a.W;
+        const int rows = a.CC * a.HH;
+        for (int row = wave; row < rows; row += 4) {
+            const int c = row / a.HH, hh = row - c * a.HH;
+            const int h = h0 + hh;
+            const bool rv = (c0 + c < a.Cg) && (h >= 0) && (h < a.H);
+            const float* src = xg + ((int64_t)c * a.H + h) * a.W;
+            float* dst = xs + c * a.PS + hh * a.WWp;
+            for (int ww = lane; ww < a.WW; ww += 64) {
+                const int w = w0 + ww;
+                dst[ww] = (rv && w >= 0 && w < a.W) ? src[w] : 0.0f;
+            }
+        }
+        // ---- stage packed weights (contiguous, float4)
+        const float4* ws4 = reinterpret_cast<const float4*>(wsrc + (int64_t)chunk * chunk_floats);
+        float4* wd4 = reinterpret_cast<float4*>(wsm);
+        for (int e = tid; e < (chunk_floats >> 2); e += kThreads) wd4[e] = ws4[e];
+        __syncthreads();
+
+        for (int r = 0; r < a.R; ++r) {
+            for (int s = 0; s < a.S; ++s) {
+                const int tap = r * a.dh * a.WWp + s * a.dw;
+                const int tbase = (r * a.S + s) * c4n;
+                for (int c4 = 0; c4 < c4n; ++c4) {
+                    const float* wrow = wsm + (tbase + c4) * MI * 64 + lane;
+                    float av[MI], bv[NJ];
+#pragma unroll
+                    for (int mi = 0; mi < MI; ++mi) av[mi] = wrow[mi * 64];
+                    const float* xrow = xs + c4 * 4 * a.PS + tap;
+#pragma unroll
+                    for (int nj = 0; nj < NJ; ++nj) bv[nj] = xrow[poff[nj]];
+#pragma unroll
+                    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+                        for (int nj = 0; nj < NJ; ++nj)
+                            acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mi], bv[nj], acc[mi][nj], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: D[row = 4*(lane>>4)+i][col = lane&15] -> y[n][k][p][q]
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+        const int slot = (wave * NJ + nj) * 16 + (lane & 15);
+        if (slot >= npix) continue;
+        const int pl = slot / a.TQ, ql = slot - pl * a.TQ;
+        const int pp = p0 + pl, qq = q0 + ql;
+        if (pp >= a.P || qq >= a.Q) continue;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int kk = kb * MI * 16 + mi * 16 + 4 * (lane >> 4) + i;
+                if (kk >= a.Kg) continue;
+                const int k = g * a.Kg + kk;
+                float v = acc[mi][nj][i];
+                if (bias) v += bias[k];
+                y[(((int64_t)n * a.K + k) * a.P + pp) * a.Q + qq] = v;
+            }
+        }
+    }
+}
+
+// Depthwise (groups == C, K = groups * Kg): one output element per lane.
+__global__ __launch_bounds__(kThreads) void conv_depthwise(const float* __restrict__ x, const float* __restrict__ qw,
+                                                           const float* __restrict__ bias, float* __restrict__ y,
+                                                           ConvArgs a) {
+    const int64_t total = (int64_t)a.N * a.K * a.P * a.Q;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total; idx += stride) {
+        int64_t t = idx;
+        const int q = (int)(t % a.Q); t /= a.Q;
+        const int p = (int)(t % a.P); t /= a.P;
+        const int k = (int)(t % a.K);
+        const int n = (int)(t / a.K);
+        const int c = k / a.Kg;  // Cg == 1
+        const float* xc = x + ((int64_t)n * a.C + c) * a.H * a.W;
+        const float* wk = qw + (int64_t)k * a.R * a.S;
+        float acc = 0.0f;
+        for (int r = 0; r < a.R; ++r) {
+            const int h = p * a.sh - a.ph + r * a.dh;
+            if (h < 0 || h >= a.H) continue;
+            for (int s = 0; s < a.S; ++s) {
+                const int w = q * a.sw - a.pw + s * a.dw;
+                if (w < 0 || w >= a.W) continue;
+                acc = fmaf(xc[(int64_t)h * a.W + w], wk[r * a.S + s], acc);
+            }
+        }
+        if (bias) acc += bias[k];
+        y[idx] = acc;
+    }
+}
+
+// ------------------------------------------------------------------ planning --
+static int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+               int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t groups, int mode,
+               int flags) {
+    (void)mode;
+    if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || K <= 0 || R <= 0 || S <= 0 || groups <= 0) {
+        set_error("po2q: all sizes must be positive");
+        return false;
+    }
+    if (sh <= 0 || sw <= 0 || dh <= 0 || dw <= 0 || ph < 0 || pw < 0) {
+        set_error("po2q: stride/dilation must be positive and padding non-negative");
+        return false;
+    }
+    if (C % groups != 0 || K % groups != 0) {
+        set_error("po2q: in_channels and out_channels must be divisible by groups");
+        return false;
+    }
+    const int64_t P = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+    const int64_t Q = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+    if (H + 2 * ph < dh * (R - 1) + 1 || W + 2 * pw < dw * (S - 1) + 1 || P <= 0 || Q <= 0) {
+        set_error("po2q: kernel size can't be greater than actual (padded) input size");
+        return false;
+    }
+    const int64_t lim = INT_MAX;
+    if (N * C > lim || N * K > lim || H * W > lim || P * Q > lim || K * (C / groups) * R * S > lim ||
+        C * H * W > lim || K * P * Q > lim) {
+        set_error("po2q: tensor too large for 32-bit per-image indexing");
+        return false;
+    }
+    if (flags == 2) {  // PO2Q_PREC_BF16X3
+        set_error("po2q: bf16x3 precision not implemented yet");
+        return false;
+    }
+    p.N = (int)N; p.C = (int)C; p.H = (int)H; p.W = (int)W; p.K = (int)K; p.R = (int)R; p.S = (int)S;
+    p.sh = (int)sh; p.sw = (int)sw; p.ph = (int)ph; p.pw = (int)pw; p.dh = (int)dh; p.dw = (int)dw;
+    p.groups = (int)groups; p.P = (int)P; p.Q = (int)Q; p.Cg = (int)(C / groups); p.Kg = (int)(K / groups);
+
+    if (p.Cg == 1 && groups > 1) {  // depthwise
+        p.kind = 1;
+        p.MI = p.NJ = 1;
+        p.TP = p.TQ = p.tilesP = p.tilesQ = 1;
+        p.CC = 1; p.nchunks = 1; p.kblocks = 1;
+        p.HH = p.WW = p.WWp = p.PS = 0; p.steps = 0;
+        p.packed_floats = (int64_t)K * R * S;
+        p.lds_bytes = 0;
+        int64_t total = (int64_t)N * K * P * Q;
+        int64_t b = (total + kThreads - 1) / kThreads;
+        p.blocks = std::min<int64_t>(std::max<int64_t>(b, 1), 65536);
+        return true;
+    }
+
+    p.kind = 0;
+    p.MI = p.Kg <= 16 ? 1 : (p.Kg <= 32 ? 2 : 4);
+    p.kblocks = ceil_div(p.Kg, 16 * p.MI);
+    // pixel tile: NJ groups of 16 pixels per wave
+    const int pix_img = p.P * p.Q;
+    p.NJ = pix_img >= 256 ? 4 : (pix_img >= 128 ? 2 : 1);
+    const int slots = 64 * p.NJ;
+    // choose TQ among candidates minimising launched slots x halo overhead
+    const int cands[] = {p.Q, 64, 56, 32, 28, 16, 8};
+    double best = 1e300;
+    for (int tq : cands) {
+        if (tq <= 0 || tq > p.Q || tq > slots) continue;
+        int tp = std::max(1, std::min(p.P, slots / tq));
+        const int tilesQ = ceil_div(p.Q, tq), tilesP = ceil_div(p.P, tp);
+        const double launched = (double)tilesQ * tilesP * slots;
+        const int hh = (tp - 1) * p.sh + (p.R - 1) * p.dh + 1;
+        const int ww = (tq - 1) * p.sw + (p.S - 1) * p.dw + 1;
+        const double halo = (double)tilesQ * tilesP * hh * ww;
+        const double cost = launched * 1.0 + halo * 0.5 * p.R * p.S / 9.0;
+        if (cost < best) { best = cost; p.TQ = tq; p.TP = tp; }
+    }
+    p.tilesQ = ceil_div(p.Q, p.TQ);
+    p.tilesP = ceil_div(p.P, p.TP);
+    p.HH = (p.TP - 1) * p.sh + (p.R - 1) * p.dh + 1;
+    p.WW = (p.TQ - 1) * p.sw + (p.S - 1) * p.dw + 1;
+    p.WWp = p.WW;
+    const int plane = p.HH * p.WWp;
+    // plane stride: lanes 16..31 read channel +1; offset it by 16 banks (stride 1)
+    // or 1 bank (stride 2: lanes already spread over even banks)
+    const int want = (p.sw == 1) ? 16 : 1;
+    p.PS = plane + ((want - plane % 32) + 32) % 32;
+    // channel chunk: multiple of 4, LDS <= 64 KiB
+    const int cg4 = ceil_div(p.Cg, 4) * 4;
+    int cc = std::min(cg4, 64);
+    auto lds_for = [&](int c) {
+        return (size_t)(c * p.PS + p.R * p.S * (c / 4) * p.MI * 64) * sizeof(float);
+    };
+    while (cc > 4 && lds_for(cc) > 64 * 1024) cc -= 4;
+    if (lds_for(cc) > 64 * 1024) {
+        set_error("po2q: conv tile does not fit in LDS (kernel too large)");
+        return false;
+    }
+    p.CC = cc;
+    p.nchunks = ceil_div(p.Cg, cc);
+    p.steps = p.R * p.S * (cc / 4);
+    p.lds_bytes = lds_for(cc);
+    p.packed_floats = (int64_t)groups * p.kblocks * p.nchunks * p.steps * p.MI * 64;
+    p.blocks = (int64_t)N * groups * p.kblocks * p.tilesP * p.tilesQ;
+    if (p.blocks > INT_MAX) {
+        set_error("po2q: grid too large");
+        return false;
+    }
+    return true;
+}
+
+template <int MI, int NJ>
+static hipError_t launch_mfma(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
+                              hipStream_t s) {
+    hipLaunchKernelGGL((conv_mfma_f32<MI, NJ>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x, packed,
+                       bias, y, to_args(p));
+    return hipGetLastError();
+}
+
+template <int MI>
+static hipError_t launch_mfma_nj(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
+                                 hipStream_t s) {
+    switch (p.NJ) {
+        case 1: return launch_mfma<MI, 1>(p, x, packed, bias, y, s);
+        case 2: return launch_mfma<MI, 2>(p, x, packed, bias, y, s);
+        default: return launch_mfma<MI, 4>(p, x, packed, bias, y, s);
+    }
+}
+
+hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
+                       hipStream_t s) {
+    if (p.kind == 1) {
+        hipLaunchKernelGGL(conv_depthwise, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
+                           to_args(p));
+        return hipGetLastError();
+    }
+    switch (p.MI) {
+        case 1: return launch_mfma_nj<1>(p, x, packed, bias, y, s);
+        case 2: return launch_mfma_nj<2>(p, x, packed, bias, y, s);
+        default: return launch_mfma_nj<4>(p, x, packed, bias, y, s);
+    }
+}
+
+}  // namespace po2q

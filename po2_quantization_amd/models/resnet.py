@@ -1,0 +1,122 @@
+"""CIFAR-style ResNet20/32/44/56 built on the drop-in QuantizedConv2d.
+
+Caller of the hot path (models/resnet.py:10-300 in the
+reference): same constructors, same module names and state_dict keys, so the
+reference's checkpoints load unchanged (after stripping DDP's "module."
+prefix, test.py:50-55).  Structure per the reference:
+  stem    3x3 conv 3->16, NOT quantized (resnet.py:99-102) + BN + ReLU
+  stages  n BasicBlocks each at 16 / 32 / 64 channels, stride 1 / 2 / 2;
+          block = qconv3x3 -> BN -> ReLU -> qconv3x3 -> BN (+ 1x1 qconv + BN
+          projection when the shape changes) -> add -> ReLU
+  head    global average pool -> Linear
+BatchNorm layers are nn.BatchNorm2d: for inference (eval) this is exactly the
+reference's nn.SyncBatchNorm, which issues no collective in eval mode.
+"""
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+
+from .quantized_conv import QuantizedConv2d
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, quantize_fn=None, bits=7):
+        super().__init__()
+        qc = dict(bias=False, quantize_fn=quantize_fn, bits=bits)
+        self.conv1 = QuantizedConv2d(inplanes, planes, 3, stride=stride, padding=1, **qc)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = QuantizedConv2d(planes, planes, 3, stride=1, padding=1, **qc)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        shortcut = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        out += shortcut
+        return self.relu(out)
+
+    def get_quantization_error(self):
+        e1, n1 = self.conv1.get_quantization_error()
+        e2, n2 = self.conv2.get_quantization_error()
+        return e1 + e2, n1 + n2
+
+
+class ResNet(nn.Module):
+    def __init__(self, block=BasicBlock, num_blocks=(3, 3, 3), num_filters=(16, 32, 64), num_classes=10,
+                 quantize_fn: Optional[Callable] = None, bits: int = 7):
+        super().__init__()
+        self.inplanes = 16
+        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(self.inplanes)
+        self.relu = nn.ReLU(inplace=True)
+        strides = (1, 2, 2)
+        for i, (planes, blocks, st) in enumerate(zip(num_filters, num_blocks, strides)):
+            setattr(self, "layer%d" % (i + 1),
+                    self._make_layer(block, planes, blocks, st, quantize_fn, bits))
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(num_filters[2] * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, block, planes, blocks, stride, quantize_fn, bits):
+        out_planes = planes * block.expansion
+        downsample = None
+        if stride != 1 or self.inplanes != out_planes:
+            downsample = nn.Sequential(
+                QuantizedConv2d(self.inplanes, out_planes, 1, stride=stride, padding=0, bias=False,
+                                quantize_fn=quantize_fn, bits=bits),
+                nn.BatchNorm2d(out_planes),
+            )
+        layers = [block(self.inplanes, planes, stride, downsample, quantize_fn=quantize_fn, bits=bits)]
+        self.inplanes = out_planes
+        layers += [block(self.inplanes, planes, quantize_fn=quantize_fn, bits=bits) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.relu(self.bn1(self.conv1(x)))
+        x = self.layer3(self.layer2(self.layer1(x)))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def get_quantization_error(self):
+        """(sum of squared quantization error, #weights) over the residual stages.
+
+        The reference (resnet.py:205-224) shadows its element counter and skips
+        the projection convs; here every block's two convs are counted once."""
+        err, num = 0.0, 0
+        for layer in (self.layer1, self.layer2, self.layer3):
+            for blk in layer:
+                if isinstance(blk, BasicBlock):
+                    e, n = blk.get_quantization_error()
+                    err, num = err + e, num + n
+        return err, num
+
+
+def _resnet(n, num_classes=10, quantize_fn=None, bits=4, **kwargs):
+    return ResNet(BasicBlock, (n, n, n), (16, 32, 64), num_classes=num_classes, quantize_fn=quantize_fn,
+                  bits=bits, **kwargs)
+
+
+def ResNet20(*, n=3, num_classes=10, quantize_fn=None, bits=4, **kwargs):
+    return _resnet(n, num_classes, quantize_fn, bits, **kwargs)
+
+
+def ResNet32(*, n=5, num_classes=10, quantize_fn=None, bits=4, **kwargs):
+    return _resnet(n, num_classes, quantize_fn, bits, **kwargs)
+
+
+def ResNet44(*, n=7, num_classes=10, quantize_fn=None, bits=4, **kwargs):
+    return _resnet(n, num_classes, quantize_fn, bits, **kwargs)
+
+
+def ResNet56(*, n=9, num_classes=10, quantize_fn=None, bits=4, **kwargs):
+    return _resnet(n, num_classes, quantize_fn, bits, **kwargs)

@@ -1,0 +1,100 @@
+"""CPU: the C-ABI library loads, exports every symbol include/po2q.h declares,
+and validates arguments on the host (no GPU work is started by these calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from po2_quantization_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "po2q.h")).read()
+    return sorted(set(re.findall(r"\b(po2q_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 6
+    for name in declared:
+        assert hasattr(L, name), name
+    assert sorted(_lib.EXPORTS) == declared
+    assert L.po2q_version().startswith(b"po2q")
+
+
+def test_quantize_rejects_empty_and_bad_args_before_launch():
+    L = _lib.load()
+    dummy = ctypes.c_void_p(16)
+    assert L.po2q_quantize_f32(dummy, dummy, 0, 4, 1, 1, dummy, 256, None) == 1
+    assert b"numel() == 0" in L.po2q_last_error()
+    assert L.po2q_quantize_f32(dummy, dummy, 10, 4, 1, 7, dummy, 256, None) == 1
+    assert b"mode" in L.po2q_last_error()
+    assert L.po2q_quantize_f32(dummy, dummy, 10, 0, 1, 1, dummy, 256, None) == 1
+    assert b"bits" in L.po2q_last_error()
+    assert L.po2q_quantize_f32(dummy, dummy, 10, 4, 1, 1, dummy, 0, None) == 3  # workspace
+
+
+CONV_ARGS = dict(N=2, C=16, H=10, W=10, K=16, R=3, S=3, sh=1, sw=1, ph=1, pw=1, dh=1, dw=1, g=1)
+
+
+def conv_call(L, over=None, mode=1, flags=0, ws_bytes=1 << 20, ptr=16):
+    a = dict(CONV_ARGS)
+    a.update(over or {})
+    p = ctypes.c_void_p(ptr)
+    args = [a[k] for k in ("N", "C", "H", "W", "K", "R", "S", "sh", "sw", "ph", "pw", "dh", "dw", "g")]
+    return L.po2q_qconv2d_f32(p, p, None, p, *args, 4, 1, mode, flags, p, ws_bytes, None)
+
+
+@pytest.mark.parametrize("over,msg", [
+    ({"C": 15, "g": 2}, b"divisible by groups"),
+    ({"H": 1, "ph": 0}, b"kernel size"),
+    ({"sh": 0}, b"stride"),
+    ({"N": 0}, b"positive"),
+])
+def test_conv_shape_validation(over, msg):
+    L = _lib.load()
+    assert conv_call(L, over) == 1
+    assert msg in L.po2q_last_error()
+
+
+def test_conv_workspace_and_mode_checks():
+    L = _lib.load()
+    assert conv_call(L, mode=9) == 1
+    assert conv_call(L, flags=7) == 1
+    assert conv_call(L, ws_bytes=8) == 3
+    assert conv_call(L, ptr=0) == 1  # null pointers
+
+
+@pytest.mark.parametrize("shape", [
+    (256, 16, 224, 224, 16, 3, 3, 1, 1, 1, 1, 1, 1, 1),   # ResNet56 stage 1 @224
+    (256, 32, 112, 112, 64, 3, 3, 2, 2, 1, 1, 1, 1, 1),   # stride-2 transition
+    (256, 32, 112, 112, 64, 1, 1, 2, 2, 0, 0, 1, 1, 1),   # 1x1 projection
+    (256, 960, 2, 2, 160, 1, 1, 1, 1, 0, 0, 1, 1, 1),     # MobileNet pointwise
+    (256, 96, 16, 16, 96, 3, 3, 1, 1, 1, 1, 1, 1, 96),    # depthwise
+])
+def test_workspace_sizes_are_small(shape):
+    L = _lib.load()
+    for mode in (0, 1, 2):
+        nbytes = L.po2q_qconv2d_workspace_bytes(*shape, mode, 0)
+        K, Cg, R, S = shape[4], shape[1] // shape[-1], shape[5], shape[6]
+        assert 0 < nbytes < 64 * K * max(Cg, 4) * R * S + 65536
+
+
+def test_cpu_tensors_raise_no_fallback():
+    import torch
+
+    from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
+    from po2_quantization_amd.utils.quantizers import PowerOfTwoQuantizer, quantizer_dict
+
+    w = torch.randn(4, 4, 3, 3)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        PowerOfTwoQuantizer.apply(w, 4)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        quantizer_dict["po2+"].forward(None, w, bits=3)
+    conv = QuantizedConv2d(4, 4, 3, quantize_fn=PowerOfTwoQuantizer, bits=4)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        conv(torch.randn(1, 4, 8, 8))

@@ -1,0 +1,150 @@
+"""GPU parity: fused quantize+conv (libpo2q) vs the reference golden vectors and
+the oracle (fp64 direct conv of the bit-exact quantized weight).
+
+Tolerance (BASELINE.md parity contract): max|y - y_ref| <= 1e-5 * max|y_ref|
+per output tensor (normwise relative, fp32 arithmetic; ties of round() follow
+torch.round = half-to-even, reproduced bit-exactly by the quantizer)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from po2_quantization_amd import _lib
+from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
+from po2_quantization_amd.utils.quantizers import quantizer_dict
+from tests._util import CONV_TOL, load_json, load_npz, normwise_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PRECISIONS = ["fp32"]
+
+
+def run_native(x, w, b, stride, pad, dil, groups, bits, mode, precision="auto"):
+    xt = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    wt = torch.from_numpy(np.ascontiguousarray(w)).to(DEV)
+    bt = torch.from_numpy(np.ascontiguousarray(b)).to(DEV) if b is not None else None
+    return _lib.qconv2d(xt, wt, bt, stride, pad, dil, groups, bits, mode, 1, precision).cpu().numpy()
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_golden_conv_vectors(precision):
+    d = load_npz("conv_kat.npz")
+    for m in load_json("conv_kat.json"):
+        n = m["name"]
+        b = d["b/" + n] if m["bias"] else None
+        y = run_native(d["x/" + n], d["w/" + n], b, m["stride"], m["pad"], m["dil"], m["groups"],
+                       m["bits"], m["mode"], precision)
+        assert y.shape == d["y/" + n].shape, n
+        assert normwise_err(y, d["y/" + n]) <= CONV_TOL, (n, normwise_err(y, d["y/" + n]))
+        assert normwise_err(y, d["y64/" + n]) <= CONV_TOL, n
+
+
+def test_golden_vectors_through_module():
+    """Same vectors through the drop-in nn.Module (ctor defaults, bias param)."""
+    d = load_npz("conv_kat.npz")
+    for m in load_json("conv_kat.json"):
+        n = m["name"]
+        qfn = None if m["mode"] == "none" else quantizer_dict[m["mode"]]
+        C, K = m["C"], m["K"]
+        mod = QuantizedConv2d(C, K, (m["R"], m["S"]), stride=m["stride"], padding=m["pad"], dilation=m["dil"],
+                              groups=m["groups"], bias=m["bias"], quantize_fn=qfn, bits=m["bits"]).to(DEV)
+        with torch.no_grad():
+            mod.weight.copy_(torch.from_numpy(d["w/" + n]))
+            if m["bias"]:
+                mod.bias.copy_(torch.from_numpy(d["b/" + n]))
+            y = mod(torch.from_numpy(d["x/" + n]).to(DEV)).cpu().numpy()
+        assert normwise_err(y, d["y/" + n]) <= CONV_TOL, n
+
+
+# ResNet56 / MobileNet conv kinds at reduced batch & spatial size vs the oracle
+SHAPES = [
+    # N, C, H, W, K, R, S, stride, pad, dil, groups
+    (2, 16, 40, 36, 16, 3, 3, 1, 1, 1, 1),
+    (2, 32, 20, 20, 32, 3, 3, 1, 1, 1, 1),
+    (1, 64, 14, 14, 64, 3, 3, 1, 1, 1, 1),
+    (2, 16, 33, 31, 32, 3, 3, 2, 1, 1, 1),
+    (2, 32, 16, 16, 64, 3, 3, 2, 1, 1, 1),
+    (2, 16, 32, 32, 32, 1, 1, 2, 0, 1, 1),
+    (2, 32, 16, 16, 64, 1, 1, 2, 0, 1, 1),
+    (2, 3, 32, 32, 16, 3, 3, 1, 1, 1, 1),
+    (2, 160, 4, 4, 960, 1, 1, 1, 0, 1, 1),
+    (2, 960, 2, 2, 160, 1, 1, 1, 0, 1, 1),
+    (2, 144, 8, 8, 144, 3, 3, 2, 1, 1, 144),
+    (2, 48, 9, 9, 24, 3, 3, 1, 1, 1, 1),
+    (1, 20, 13, 11, 36, 3, 3, 1, 2, 2, 2),
+    (1, 8, 70, 70, 24, 3, 3, 1, 1, 1, 1),
+    (3, 16, 8, 8, 16, 3, 3, 1, 1, 1, 1),
+    (1, 12, 9, 9, 20, 5, 3, 2, (2, 1), 1, 4),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+", "none"])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_shapes_vs_oracle(shape, mode, precision):
+    N, C, H, W, K, R, S, st, pad, dil, groups = shape
+    g = torch.Generator().manual_seed(hash(shape) & 0xFFFF)
+    x = torch.randn(N, C, H, W, generator=g).numpy()
+    w = (torch.randn(K, C // groups, R, S, generator=g) * 0.2).numpy()
+    b = (torch.randn(K, generator=g) * 0.1).numpy() if K % 3 == 0 else None
+    y = run_native(x, w, b, st, pad, dil, groups, 4, mode, precision)
+    ref, _ = O.qconv2d(x, w, b, st, pad, dil, groups, 4, mode)
+    assert y.shape == ref.shape
+    assert normwise_err(y, ref) <= CONV_TOL, normwise_err(y, ref)
+
+
+def test_full_size_resnet56_stage1_vs_torch_fp32():
+    """BASELINE size (bs=256, 224x224, 16->16): against torch's own fp32 GPU conv of
+    the bit-exact quantized weight (a plain PyTorch fp32 reference of the same op)."""
+    torch.manual_seed(0)
+    x = torch.randn(256, 16, 224, 224, device=DEV)
+    w = torch.randn(16, 16, 3, 3, device=DEV) * 0.1
+    y = _lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, "po2")
+    qw = _lib.quantize(w, 4, "po2")
+    ref = torch.nn.functional.conv2d(x, qw, None, 1, 1)
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    assert err <= CONV_TOL, err
+    # spot-check images at both ends of the batch against the fp64 oracle as well
+    idx = [0, 1, 254, 255]
+    o, _ = O.qconv2d(x[idx].cpu().numpy(), w.cpu().numpy(), None, 1, 1, 1, 1, 4, "po2")
+    assert normwise_err(y[idx].cpu().numpy(), o) <= CONV_TOL
+
+
+def test_backward_matches_torch_ste():
+    torch.manual_seed(1)
+    x = torch.randn(4, 16, 12, 12, device=DEV, requires_grad=True)
+    mod = QuantizedConv2d(16, 32, 3, stride=2, bias=True, quantize_fn=quantizer_dict["po2"], bits=4).to(DEV)
+    y = mod(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    x2 = x.detach().clone().requires_grad_(True)
+    w2 = mod.weight.detach().clone().requires_grad_(True)
+    b2 = mod.bias.detach().clone().requires_grad_(True)
+    qw = w2 + (_lib.quantize(w2.detach(), 4, "po2") - w2).detach()  # STE
+    y2 = torch.nn.functional.conv2d(x2, qw, b2, 2, 1)
+    y2.backward(gy)
+    assert torch.allclose(y, y2, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(mod.weight.grad, w2.grad, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(mod.bias.grad, b2.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_errors_match_reference_behaviour():
+    x = torch.randn(1, 5, 8, 8, device=DEV)
+    with pytest.raises(RuntimeError, match="channels"):
+        _lib.qconv2d(x, torch.randn(4, 4, 3, 3, device=DEV), None, 1, 1, 1, 1, 4, "po2")
+    with pytest.raises(RuntimeError, match="kernel size"):
+        _lib.qconv2d(torch.randn(1, 4, 2, 2, device=DEV), torch.randn(4, 4, 5, 5, device=DEV), None,
+                     1, 0, 1, 1, 4, "po2")
+    with pytest.raises(RuntimeError, match="float32"):
+        _lib.qconv2d(x.double(), torch.randn(4, 5, 3, 3, device=DEV), None, 1, 1, 1, 1, 4, "po2")
+
+
+def test_weight_special_values():
+    """all-zero weights -> NaN output (0/0 in the reference quantizer); NaN weight -> NaN."""
+    x = torch.randn(1, 4, 6, 6, device=DEV)
+    y = _lib.qconv2d(x, torch.zeros(4, 4, 3, 3, device=DEV), None, 1, 1, 1, 1, 4, "po2")
+    assert torch.isnan(y).all()
+    w = torch.randn(4, 4, 3, 3, device=DEV)
+    w[0, 0, 0, 0] = float("nan")
+    assert torch.isnan(_lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, "po2+")).all()

@@ -1,0 +1,59 @@
+"""GPU parity at model level: the drop-in modules inside the reference's model
+graphs reproduce the reference's logits (golden vectors from running the
+reference models on CPU, tests/golden/gen_golden.py) on identical weights."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from po2_quantization_amd.models.model import get_model
+from po2_quantization_amd.utils.quantizers import quantize_model, quantizer_dict
+from tests._util import CONV_TOL, GOLDEN, load_npz, normwise_err
+
+sys.path.insert(0, GOLDEN)
+from fill import seeded_fill_  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+# logits go through ~57 conv layers + BN; per-layer normwise error ~1e-7 → allow 1e-5 on logits
+LOGIT_TOL = CONV_TOL
+
+
+def build(mt, q, bits):
+    m = get_model(mt, 10, quantizer_dict[q] if q else None, bits, 32)
+    seeded_fill_(m, seed=7)
+    return m.to(DEV).eval()
+
+
+@pytest.mark.parametrize("mt,q,bits", [("resnet20", None, 4), ("resnet56", "po2", 4), ("resnet20", "po2+", 3)])
+def test_qat_mode_logits(mt, q, bits):
+    d = load_npz("models.npz")
+    m = build(mt, q, bits)
+    with torch.no_grad():
+        y = m(torch.from_numpy(d["x/cifar8"]).to(DEV)).cpu().numpy()
+    ref = d["logits/%s/%s/%d" % (mt, q or "none", bits)]
+    assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
+
+
+@pytest.mark.parametrize("qn", ["po2", "po2+", "lin", "lin+"])
+def test_ptq_config1_resnet20(qn):
+    """Config 1 (test.py PTQ path): quantize_model(model, quantizer, 4) then eval."""
+    d = load_npz("models.npz")
+    m = build("resnet20", None, 4)
+    err = quantize_model(m, quantizer_dict[qn], 4)
+    ref_err = float(d["ptq_err/resnet20/%s/4" % qn])
+    assert abs(err - ref_err) <= 1e-5 * ref_err, (err, ref_err)
+    with torch.no_grad():
+        y = m(torch.from_numpy(d["x/cifar8"]).to(DEV)).cpu().numpy()
+    assert normwise_err(y, d["ptq_logits/resnet20/%s/4" % qn]) <= LOGIT_TOL
+
+
+def test_state_dict_keys_match_reference():
+    import json
+
+    keys = json.load(open(os.path.join(GOLDEN, "models.json")))
+    for mt in ("resnet20", "resnet56"):
+        m = get_model(mt, 10, None, 4, 32)
+        assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == keys[mt]
