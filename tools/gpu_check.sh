@@ -1,0 +1,36 @@
+#!/bin/bash
+# GPU-box check sequence (run through gpurun).  Every GPU step has its own time
+# limit; a crash / abort / timeout (exit code > 1) ends the script right there.
+# Usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench layers prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${*:-smoke tests bench}
+
+run() {  # name timeout cmd...
+    local name=$1 t=$2
+    shift 2
+    local t0=$(date +%s)
+    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a gpurun_out/status.txt
+    tail -n 5 "gpurun_out/$name.log"
+    if [ $rc -gt 1 ]; then
+        echo "stopping: $name exited with $rc"
+        exit $rc
+    fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+        bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        layers) run layers 600 python tools/layer_bench.py --torch ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+                  -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $s" ;;
+    esac
+done
