@@ -28,9 +28,11 @@ enum po2q_mode { PO2Q_MODE_NONE = 0, PO2Q_MODE_PO2 = 1, PO2Q_MODE_PO2_PLUS = 2 }
 
 /* conv arithmetic (flags of po2q_qconv2d_f32) */
 enum po2q_precision {
-    PO2Q_PREC_AUTO = 0,   /* library default (currently PO2Q_PREC_FP32) */
-    PO2Q_PREC_FP32 = 1,   /* fp32-input MFMA, exact fp32 fma chain */
-    PO2Q_PREC_BF16X3 = 2  /* bf16 MFMA, activations split hi+mid+lo (exact), weights 2^e (exact) */
+    PO2Q_PREC_AUTO = 0,   /* BF16X3 when eligible (po2/po2+ weights, groups == 1), else FP32 */
+    PO2Q_PREC_FP32 = 1,   /* fp32-input MFMA, exact fp32 fma chain (any weights) */
+    PO2Q_PREC_BF16X3 = 2  /* bf16 MFMA on exact operands: weights Q(w)/scale = +-2^e, activations
+                             split by truncation into hi+mid+lo bf16 (exact); fp32 accumulation.
+                             PO2Q_ERR_UNSUPPORTED when not eligible. */
 };
 
 enum po2q_status {
@@ -64,12 +66,14 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
  * mode PO2Q_MODE_NONE is the plain conv of quantize_fn=None (:37-38).
  * x [N, C, H, W], w [K, C/groups, R, S], bias [K] or NULL, y [N, K, P, Q] with
  * P = (H + 2*pad_h - dil_h*(R-1) - 1)/stride_h + 1 (likewise Q).
- * flags: one of enum po2q_precision.
+ * flags: one of enum po2q_precision.  The workspace size depends on every
+ * argument of po2q_qconv2d_workspace_bytes (the plan is chosen from them).
  */
 size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W,
                                     int64_t K, int64_t R, int64_t S,
                                     int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
-                                    int64_t dil_h, int64_t dil_w, int64_t groups, int mode, int flags);
+                                    int64_t dil_h, int64_t dil_w, int64_t groups,
+                                    int bits, int fsr, int mode, int flags);
 int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y,
                      int64_t N, int64_t C, int64_t H, int64_t W,
                      int64_t K, int64_t R, int64_t S,
@@ -77,6 +81,17 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
                      int64_t dil_h, int64_t dil_w, int64_t groups,
                      int bits, int fsr, int mode, int flags,
                      void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Diagnostic: the plan po2q_qconv2d_f32 would run for these arguments, as a
+ * NUL-terminated text ("kind=bf16x3 CC=16 NT=1 NJ=4 tile=8x32 ..."), written
+ * to buf (truncated to len).  No reference counterpart; used by bench.py and
+ * tests to name the kernel that was measured.
+ */
+int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                          int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                          int64_t dil_h, int64_t dil_w, int64_t groups,
+                          int bits, int fsr, int mode, int flags, char* buf, size_t len);
 
 #ifdef __cplusplus
 }

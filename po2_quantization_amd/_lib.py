@@ -25,6 +25,7 @@ EXPORTS = (
     "po2q_quantize_f32",
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
+    "po2q_qconv2d_describe",
 )
 
 _lib = None
@@ -55,9 +56,11 @@ def load():
     L.po2q_quantize_f32.restype = i32
     L.po2q_quantize_f32.argtypes = [p, p, i64, i32, i32, i32, p, sz, p]
     L.po2q_qconv2d_workspace_bytes.restype = sz
-    L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32]
+    L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32, i32, i32]
     L.po2q_qconv2d_f32.restype = i32
     L.po2q_qconv2d_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+    L.po2q_qconv2d_describe.restype = i32
+    L.po2q_qconv2d_describe.argtypes = [i64] * 14 + [i32, i32, i32, i32, ctypes.c_char_p, sz]
     _lib = L
     return L
 
@@ -135,7 +138,7 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
     wc = w.contiguous()
     bc = bias.contiguous() if bias is not None else None
     with torch.cuda.device(xc.device):
-        nbytes = L.po2q_qconv2d_workspace_bytes(*args, mode_id, prec)
+        nbytes = L.po2q_qconv2d_workspace_bytes(*args, int(bits), int(fsr), mode_id, prec)
         if nbytes == 0:
             _check(1)
         y = torch.empty((N, K, max(P, 0), max(Q, 0)), dtype=torch.float32, device=xc.device)
@@ -144,3 +147,16 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
                                   y.data_ptr(), *args, int(bits), int(fsr), mode_id, prec,
                                   ws.data_ptr(), ws.numel(), _stream(xc.device)))
     return y
+
+
+def describe(N, C, H, W, K, R, S, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+             precision="auto"):
+    """The kernel plan qconv2d would run for this shape (diagnostic text)."""
+    L = load()
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    dh, dw = _pair(dilation)
+    buf = ctypes.create_string_buffer(512)
+    _check(L.po2q_qconv2d_describe(N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, int(groups), int(bits), int(fsr),
+                                   MODES[mode], PRECISIONS[precision], buf, 512))
+    return buf.value.decode()

@@ -3,6 +3,7 @@
 // here allocates device memory or synchronises.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -75,14 +76,33 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
     return hip_status(launch_quantize_plain(w, n, partial, nb, bits, fsr, mode, out, s), "quantize launch");
 }
 
-size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
-                                    int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h,
-                                    int64_t dil_w, int64_t groups, int mode, int flags) {
-    ConvPlan p;
-    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, flags))
-        return 0;
+// Workspace layout: [absmax partials][scale (bf16x3)][packed weights]
+struct WsLayout {
+    size_t part_bytes, scale_off, packed_off, total;
+    int nparts;  // 0: absmax fused into the bf16x3 pack kernel
+};
+
+static WsLayout ws_layout(const ConvPlan& p, int mode) {
+    WsLayout L;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    return align_up((size_t)absmax_blocks(nw) * sizeof(unsigned)) + align_up((size_t)p.packed_floats * sizeof(float));
+    const bool fused = p.kind == KIND_BF16X3 && nw <= kFusedAbsmaxMax;
+    L.nparts = (mode == PO2Q_MODE_NONE || fused) ? 0 : absmax_blocks(nw);
+    L.part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
+    L.scale_off = L.part_bytes;
+    L.packed_off = L.scale_off + kAlign;
+    L.total = L.packed_off + align_up((size_t)p.packed_floats * sizeof(float));
+    return L;
+}
+
+size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                                       int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                                       int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode,
+                                       int flags) {
+    ConvPlan p;
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
+                   flags))
+        return 0;
+    return ws_layout(p, mode).total;
 }
 
 int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
@@ -99,27 +119,58 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
         return PO2Q_ERR_INVALID;
     }
     ConvPlan p;
-    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, flags))
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
+                   flags))
         return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
-    const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    const size_t part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
-    const size_t need = part_bytes + align_up((size_t)p.packed_floats * sizeof(float));
-    if (workspace_bytes < need) {
-        set_error("po2q: conv workspace too small (need " + std::to_string(need) + " bytes)");
+    const WsLayout L = ws_layout(p, mode);
+    if (workspace_bytes < L.total) {
+        set_error("po2q: conv workspace too small (need " + std::to_string(L.total) + " bytes)");
         return PO2Q_ERR_WORKSPACE;
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    unsigned* partial = reinterpret_cast<unsigned*>(workspace);
-    float* packed = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + part_bytes);
-    const int nb = absmax_blocks(nw);
+    char* ws = reinterpret_cast<char*>(workspace);
+    unsigned* partial = reinterpret_cast<unsigned*>(ws);
+    float* scale = reinterpret_cast<float*>(ws + L.scale_off);
+    void* packed = ws + L.packed_off;
+    const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
     int st;
-    if (mode != PO2Q_MODE_NONE) {
-        st = hip_status(launch_absmax(w, nw, partial, nb, s), "absmax launch");
+    if (L.nparts > 0) {
+        st = hip_status(launch_absmax(w, nw, partial, L.nparts, s), "absmax launch");
         if (st) return st;
     }
-    st = hip_status(launch_pack_weights(p, w, partial, nb, bits, fsr, mode, packed, s), "weight pack launch");
+    if (p.kind == KIND_BF16X3) {
+        st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
+                                           reinterpret_cast<uint16_t*>(packed), scale, s),
+                        "weight pack launch");
+        if (st) return st;
+        return hip_status(launch_conv_bf16x3(p, x, reinterpret_cast<const uint16_t*>(packed), scale, bias, y, s),
+                          "conv launch");
+    }
+    st = hip_status(launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
+                    "weight pack launch");
     if (st) return st;
-    return hip_status(launch_conv(p, x, packed, bias, y, s), "conv launch");
+    return hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
+}
+
+int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                          int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h,
+                          int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags, char* buf,
+                          size_t len) {
+    ConvPlan p;
+    if (!buf || len == 0) {
+        set_error("po2q: describe needs a buffer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
+                   flags))
+        return PO2Q_ERR_INVALID;
+    static const char* kinds[] = {"mfma_f32", "depthwise", "bf16x3"};
+    snprintf(buf, len,
+             "kind=%s CC=%d NT=%d MI=%d NJ=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
+             "lds=%zu blocks=%lld",
+             kinds[p.kind], p.CC, p.NT, p.MI, p.NJ, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW, p.nchunks, p.kblocks,
+             p.steps, p.lds_bytes, (long long)p.blocks);
+    return PO2Q_OK;
 }
 
 }  // extern "C"

@@ -180,8 +180,7 @@ static int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
                int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t groups, int mode,
-               int flags) {
-    (void)mode;
+               int bits, int fsr, int flags) {
     if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || K <= 0 || R <= 0 || S <= 0 || groups <= 0) {
         set_error("po2q: all sizes must be positive");
         return false;
@@ -206,16 +205,22 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
         set_error("po2q: tensor too large for 32-bit per-image indexing");
         return false;
     }
-    if (flags == 2) {  // PO2Q_PREC_BF16X3
-        set_error("po2q: bf16x3 precision not implemented yet");
-        return false;
-    }
     p.N = (int)N; p.C = (int)C; p.H = (int)H; p.W = (int)W; p.K = (int)K; p.R = (int)R; p.S = (int)S;
     p.sh = (int)sh; p.sw = (int)sw; p.ph = (int)ph; p.pw = (int)pw; p.dh = (int)dh; p.dw = (int)dw;
     p.groups = (int)groups; p.P = (int)P; p.Q = (int)Q; p.Cg = (int)(C / groups); p.Kg = (int)(K / groups);
 
+    p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S;
+    // bf16x3 split-exact MFMA (po2q_conv_x3.hip): default for quantized weights
+    if (flags == 2 || (flags == 0 && mode != 0 && !(p.Cg == 1 && groups > 1))) {
+        if (plan_bf16x3(p, mode, bits, fsr)) return true;
+        if (flags == 2) {
+            set_error("po2q: bf16x3 precision needs power-of-two weights (mode po2/po2+, exponents within the "
+                      "bf16 range) and groups == 1");
+            return false;
+        }
+    }
     if (p.Cg == 1 && groups > 1) {  // depthwise
-        p.kind = 1;
+        p.kind = KIND_DEPTHWISE;
         p.MI = p.NJ = 1;
         p.TP = p.TQ = p.tilesP = p.tilesQ = 1;
         p.CC = 1; p.nchunks = 1; p.kblocks = 1;
@@ -228,7 +233,7 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
         return true;
     }
 
-    p.kind = 0;
+    p.kind = KIND_MFMA_F32;
     p.MI = p.Kg <= 16 ? 1 : (p.Kg <= 32 ? 2 : 4);
     p.kblocks = ceil_div(p.Kg, 16 * p.MI);
     // pixel tile: NJ groups of 16 pixels per wave
@@ -303,7 +308,7 @@ static hipError_t launch_mfma_nj(const ConvPlan& p, const float* x, const float*
 
 hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
                        hipStream_t s) {
-    if (p.kind == 1) {
+    if (p.kind == KIND_DEPTHWISE) {
         hipLaunchKernelGGL(conv_depthwise, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
                            to_args(p));
         return hipGetLastError();

@@ -12,6 +12,7 @@ void set_error(const std::string& msg);
 
 constexpr int kThreads = 256;          // 4 waves of 64
 constexpr int kMaxPartials = 1024;     // absmax partials (blocks of the reduction pass)
+constexpr int64_t kFusedAbsmaxMax = 1 << 20;  // weights up to this size: absmax fused into the pack kernel
 
 // ---------------------------------------------------------------- quantizer --
 // Number of partial-max slots the reduction pass uses for an n-element tensor.
@@ -24,32 +25,52 @@ hipError_t launch_absmax(const float* w, int64_t n, unsigned* partial, int block
 hipError_t launch_quantize_plain(const float* w, int64_t n, const unsigned* partial, int nparts,
                                  int bits, int fsr, int mode, float* out, hipStream_t s);
 
+// Conv kinds
+enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2 };
+
 // Conv geometry and tiling plan (host-side, shared by workspace sizing and launch).
 struct ConvPlan {
     // problem
     int N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups;
     int P, Q, Cg, Kg;
     // kernel choice
-    int kind;      // 0 = MFMA fp32 implicit GEMM, 1 = depthwise direct, 2 = bf16x3 MFMA
-    int MI, NJ;    // 16-channel groups per block, 16-pixel groups per wave
+    int kind;
+    int MI, NJ;    // fp32: 16-channel groups per block / 16-pixel groups per wave; bf16x3: NJ = pixel groups per wave
+    int NT;        // bf16x3: 16-wide output-channel tiles per wave (K block = 16*NT)
     int TP, TQ, tilesP, tilesQ;  // output pixel tile
     int CC, nchunks, kblocks;    // channel chunk, #chunks, #output-channel blocks per group
-    int HH, WW, WWp, PS;         // LDS halo tile dims / row stride / plane stride (floats)
-    int steps;                   // MFMA steps per chunk = R*S*CC/4
-    int64_t packed_floats;       // packed weight buffer (floats)
+    int HH, WW, WWp, PS;         // LDS halo tile dims / row stride / plane stride (floats, fp32 kind)
+    int steps;                   // MFMA k-steps per chunk
+    int SB;                      // bf16x3: LDS bytes per halo pixel (per split plane)
+    int plane;                   // bf16x3: bytes per split plane (halo + 16 B zero pad)
+    int taps;                    // R*S
+    int64_t packed_floats;       // packed weight buffer (4-byte words)
     size_t lds_bytes;
     int64_t blocks;
 };
 
 bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-               int64_t groups, int mode, int flags);
+               int64_t groups, int mode, int bits, int fsr, int flags);
+
+// bf16x3 planner (po2q_conv_x3.hip): fills the bf16x3 fields of an already
+// validated plan; false if the shape / exponent range is not eligible.
+bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr);
 
 // Pack (and quantize unless mode == 0) the weight into the plan's layout.
 hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned* partial, int nparts,
                                int bits, int fsr, int mode, float* packed, hipStream_t s);
 
+// bf16x3: quantize + pack weights as exact bf16 +-2^e fragments, write the
+// scale multiplier to *scale_out.  nparts == 0: absmax is reduced in-kernel.
+hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned* partial, int nparts,
+                              int bits, int fsr, int mode, uint16_t* packed, float* scale_out,
+                              hipStream_t s);
+
 hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, const float* bias,
                        float* y, hipStream_t s);
+
+hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t* packed,
+                              const float* scale, const float* bias, float* y, hipStream_t s);
 
 }  // namespace po2q

@@ -132,6 +132,102 @@ __global__ __launch_bounds__(kThreads) void pack_mfma_f32_kernel(const float* __
     }
 }
 
+// bf16x3 layout (plan kind 2): packed[kb][chunk][ks][nt][lane][e] (uint16) =
+//   B fragment of v_mfma_f32_16x16x32_bf16: lane l holds B[k = 8*(l>>4) + e][n = l&15];
+//   n -> output channel kb*16*NT + nt*16 + (l&15); the k-step's 4 channel octets
+//   oi = ks*4 + (l>>4) map tap-major to (tap = oi / (CC/8), channels (oi % (CC/8))*8 + e).
+// Value: W' = Q(w) / scale = sign(w) * 2^e exactly (bf16), 0 for padding.  When
+// scale is not a positive finite number (all-zero / NaN / inf weights) the
+// reference's Q(w) itself (NaN / inf / 0) is stored and the multiplier is 1.
+struct PackX3 {
+    int C, K, R, S, CC, NT, nchunks, ksteps, taps;
+    int64_t total;  // uint16 elements
+};
+
+__device__ __forceinline__ uint16_t bf16_bits_keep_nan(float q) {
+    const uint32_t u = __float_as_uint(q);
+    const bool nan = ((u & 0x7f800000u) == 0x7f800000u) && (u & 0x007fffffu);
+    return (uint16_t)((u >> 16) | (nan ? 0x40u : 0u));
+}
+
+__global__ __launch_bounds__(kThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
+                                                               const unsigned* __restrict__ partial,
+                                                               int nparts, int lo, int hi, int mode,
+                                                               PackX3 pg, uint16_t* __restrict__ packed,
+                                                               float* __restrict__ scale_out) {
+    __shared__ unsigned red4[4];
+    unsigned m = 0u;
+    if (nparts > 0) {
+        for (int i = threadIdx.x; i < nparts; i += kThreads) m = max(m, partial[i]);
+    } else {  // fused absmax: every block reduces the whole (small, L2-resident) weight tensor
+        const bool aligned = ((reinterpret_cast<uintptr_t>(w) & 15u) == 0);
+        int64_t i0 = 0;
+        if (aligned) {
+            const int64_t n4 = n >> 2;
+            const float4* w4 = reinterpret_cast<const float4*>(w);
+            for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+                const float4 v = w4[i];
+                const unsigned a = __float_as_uint(v.x) & 0x7fffffffu, b = __float_as_uint(v.y) & 0x7fffffffu;
+                const unsigned c = __float_as_uint(v.z) & 0x7fffffffu, d = __float_as_uint(v.w) & 0x7fffffffu;
+                m = max(m, max(max(a, b), max(c, d)));
+            }
+            i0 = n4 << 2;
+        }
+        for (int64_t i = i0 + threadIdx.x; i < n; i += kThreads) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+    }
+    m = block_max_u32(m, red4);
+    const float scale = __uint_as_float(m);
+    const bool fin = (m > 0u) && (m < 0x7f800000u);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = fin ? scale : 1.0f;
+    const int OCT = pg.CC >> 3;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < pg.total; j += stride) {
+        int64_t t = j;
+        const int e8 = (int)(t & 7); t >>= 3;
+        const int lane = (int)(t & 63); t >>= 6;
+        const int nt = (int)(t % pg.NT); t /= pg.NT;
+        const int ks = (int)(t % pg.ksteps); t /= pg.ksteps;
+        const int chunk = (int)(t % pg.nchunks);
+        const int kb = (int)(t / pg.nchunks);
+        const int k = kb * 16 * pg.NT + nt * 16 + (lane & 15);
+        const int oi = ks * 4 + (lane >> 4);
+        const int tap = oi / OCT;
+        const int c = chunk * pg.CC + (oi - tap * OCT) * 8 + e8;
+        uint16_t v = 0;
+        if (k < pg.K && c < pg.C && tap < pg.taps) {
+            const int r = tap / pg.S, s = tap - (tap / pg.S) * pg.S;
+            const float wv = w[(((int64_t)k * pg.C + c) * pg.R + r) * pg.S + s];
+            if (fin) {
+                int e = 0;
+                exponent_of(wv, scale, mode, lo, hi, e);  // finite: a = |w/scale| <= 1
+                const float sg = ref_sign(wv);
+                v = (sg == 0.0f) ? (uint16_t)0
+                                 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
+            } else {
+                v = bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
+            }
+        }
+        packed[j] = v;
+    }
+}
+
+hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned* partial, int nparts, int bits,
+                              int fsr, int mode, uint16_t* packed, float* scale_out, hipStream_t s) {
+    int lo, hi;
+    clamp_window(bits, fsr, lo, hi);
+    PackX3 pg;
+    pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
+    pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps;
+    pg.total = p.packed_floats * 2;
+    int64_t b = (pg.total + 2047) / 2048;
+    if (b < 1) b = 1;
+    if (b > 40) b = 40;
+    const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
+    hipLaunchKernelGGL(pack_bf16x3_kernel, dim3((unsigned)b), dim3(kThreads), 0, s, w, n, partial, nparts, lo, hi,
+                       mode - 1, pg, packed, scale_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned* partial, int nparts, int bits,
                                int fsr, int mode, float* packed, hipStream_t s) {
     int lo = 0, hi = 0;

@@ -79,7 +79,7 @@ def test_conv_workspace_and_mode_checks():
 def test_workspace_sizes_are_small(shape):
     L = _lib.load()
     for mode in (0, 1, 2):
-        nbytes = L.po2q_qconv2d_workspace_bytes(*shape, mode, 0)
+        nbytes = L.po2q_qconv2d_workspace_bytes(*shape, 4, 1, mode, 0)
         K, Cg, R, S = shape[4], shape[1] // shape[-1], shape[5], shape[6]
         assert 0 < nbytes < 64 * K * max(Cg, 4) * R * S + 65536
 
@@ -98,3 +98,21 @@ def test_cpu_tensors_raise_no_fallback():
     conv = QuantizedConv2d(4, 4, 3, quantize_fn=PowerOfTwoQuantizer, bits=4)
     with pytest.raises(RuntimeError, match="HIP device"):
         conv(torch.randn(1, 4, 8, 8))
+
+
+def test_bf16x3_eligibility_on_host():
+    """bf16x3 needs power-of-two weights: mode none / grouped convs / exponent
+    windows outside the bf16 range are rejected (or, under AUTO, planned fp32)."""
+    L = _lib.load()
+    shape = (2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    for bits, fsr, mode, flags, ok in [
+        (4, 1, 1, 2, True), (4, 1, 2, 2, True), (7, 1, 1, 2, True),
+        (4, 1, 0, 2, False),      # plain conv: weights not exact in bf16
+        (8, 1, 1, 2, False),      # exponents down to -127: below the bf16 normal range
+        (4, 1, 0, 0, True), (8, 1, 1, 0, True),  # AUTO falls back to fp32
+    ]:
+        nbytes = L.po2q_qconv2d_workspace_bytes(*shape, bits, fsr, mode, flags)
+        assert (nbytes > 0) == ok, (bits, fsr, mode, flags)
+    grouped = (2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 2)
+    assert L.po2q_qconv2d_workspace_bytes(*grouped, 4, 1, 1, 2) == 0
+    assert b"bf16x3" in L.po2q_last_error()

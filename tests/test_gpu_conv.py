@@ -16,7 +16,11 @@ from tests._util import CONV_TOL, load_json, load_npz, normwise_err
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-PRECISIONS = ["fp32"]
+PRECISIONS = ["auto", "fp32", "bf16x3"]
+
+
+def eligible_x3(mode, groups, bits=4):
+    return mode != "none" and groups == 1 and bits <= 7
 
 
 def run_native(x, w, b, stride, pad, dil, groups, bits, mode, precision="auto"):
@@ -31,6 +35,8 @@ def test_golden_conv_vectors(precision):
     d = load_npz("conv_kat.npz")
     for m in load_json("conv_kat.json"):
         n = m["name"]
+        if precision == "bf16x3" and not eligible_x3(m["mode"], m["groups"], m["bits"]):
+            continue
         b = d["b/" + n] if m["bias"] else None
         y = run_native(d["x/" + n], d["w/" + n], b, m["stride"], m["pad"], m["dil"], m["groups"],
                        m["bits"], m["mode"], precision)
@@ -87,26 +93,38 @@ def test_shapes_vs_oracle(shape, mode, precision):
     x = torch.randn(N, C, H, W, generator=g).numpy()
     w = (torch.randn(K, C // groups, R, S, generator=g) * 0.2).numpy()
     b = (torch.randn(K, generator=g) * 0.1).numpy() if K % 3 == 0 else None
+    if precision == "bf16x3" and not eligible_x3(mode, groups):
+        with pytest.raises(RuntimeError, match="bf16x3"):
+            run_native(x, w, b, st, pad, dil, groups, 4, mode, precision)
+        return
     y = run_native(x, w, b, st, pad, dil, groups, 4, mode, precision)
     ref, _ = O.qconv2d(x, w, b, st, pad, dil, groups, 4, mode)
     assert y.shape == ref.shape
     assert normwise_err(y, ref) <= CONV_TOL, normwise_err(y, ref)
 
 
-def test_full_size_resnet56_stage1_vs_torch_fp32():
-    """BASELINE size (bs=256, 224x224, 16->16): against torch's own fp32 GPU conv of
+FULL_LAYERS = [  # BASELINE config (bs=256, 224x224): every distinct ResNet56 qconv shape
+    (16, 224, 16, 3, 1, 1), (16, 224, 32, 3, 2, 1), (16, 224, 32, 1, 2, 0), (32, 112, 32, 3, 1, 1),
+    (32, 112, 64, 3, 2, 1), (32, 112, 64, 1, 2, 0), (64, 56, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("layer", FULL_LAYERS, ids=[str(l) for l in FULL_LAYERS])
+def test_full_size_resnet56_layers_vs_torch_fp32(layer):
+    """BASELINE size (bs=256, 224x224 input): against torch's own fp32 GPU conv of
     the bit-exact quantized weight (a plain PyTorch fp32 reference of the same op)."""
+    C, H, K, R, st, pad = layer
     torch.manual_seed(0)
-    x = torch.randn(256, 16, 224, 224, device=DEV)
-    w = torch.randn(16, 16, 3, 3, device=DEV) * 0.1
-    y = _lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, "po2")
+    x = torch.randn(256, C, H, H, device=DEV)
+    w = torch.randn(K, C, R, R, device=DEV) * 0.1
+    y = _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2")
     qw = _lib.quantize(w, 4, "po2")
-    ref = torch.nn.functional.conv2d(x, qw, None, 1, 1)
+    ref = torch.nn.functional.conv2d(x, qw, None, st, pad)
     err = ((y - ref).abs().max() / ref.abs().max()).item()
     assert err <= CONV_TOL, err
     # spot-check images at both ends of the batch against the fp64 oracle as well
-    idx = [0, 1, 254, 255]
-    o, _ = O.qconv2d(x[idx].cpu().numpy(), w.cpu().numpy(), None, 1, 1, 1, 1, 4, "po2")
+    idx = [0, 255]
+    o, _ = O.qconv2d(x[idx].cpu().numpy(), w.cpu().numpy(), None, st, pad, 1, 1, 4, "po2")
     assert normwise_err(y[idx].cpu().numpy(), o) <= CONV_TOL
 
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box check sequence (run through gpurun).  Every GPU step has its own time
 # limit; a crash / abort / timeout (exit code > 1) ends the script right there.
-# Usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench layers prof pmc
+# Usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench layers sweep prof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -29,6 +29,7 @@ for s in $STEPS; do
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
+        sweep) run sweep 900 python tools/tile_sweep.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
                   -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s" ;;
