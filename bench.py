@@ -212,7 +212,11 @@ def main():
     avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
     _, C, K, R, st, pad, _ = chain.layers[chain.timed_layer]
     flops, nbytes = conv_work(B, C, Hs, K, R, st, pad)
-    prec = "fp32" if args.precision == "auto" else args.precision
+    # the conv arithmetic the library actually planned for this layer (AUTO picks
+    # bf16x3 for power-of-two weights): three exact bf16 MFMA passes per fp32 product
+    plan = _lib.describe(B, C, Hs, Hs, K, R, R, st, pad, 1, 1, args.bits,
+                         None if args.quantizer == "none" else args.quantizer, 1, args.precision)
+    prec = "bf16x3" if "kind=bf16x3" in plan else "fp32"
     if prec == "bf16x3":
         peak_c = PEAK_BF16_MFMA_TFLOPS / 3.0
     else:
@@ -230,12 +234,12 @@ def main():
     traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(traffic_file):
         try:
-            tr = json.load(open(traffic_file)).get("%s/%s/%d" % (prec, args.model, Hs))
-            roof["traffic"] = tr
+            tr = json.load(open(traffic_file)).get(plan)
+            roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
         except (ValueError, OSError):
             pass
-    roof.update({"kernel": "fused po2 quantize+conv 3x3 %d->%d @%dx%d bs=%d (absmax+pack+conv launches)"
-                           % (C, K, Hs, Hs, B),
+    roof.update({"kernel": "fused %s quantize+conv %dx%d %d->%d @%dx%d bs=%d (pack + conv launches): %s"
+                           % (args.quantizer, R, R, C, K, Hs, Hs, B, plan),
                  "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(nbytes), "flops": int(flops)})
 
     images = world * B * args.steps
@@ -243,7 +247,7 @@ def main():
         "metric": METRIC, "value": round(images / dt, 2), "unit": "images/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3-split MFMA)", "data": "synthetic",
+        "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
         "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
                                   " + RCCL all_gather(logits)" if world > 1 else ""),

@@ -54,6 +54,7 @@ struct X3Args {
     int vec;       // float4 epilogue allowed (Q % 4 == 0 && TQ % 4 == 0)
     int remap;     // XCD-aware block remap (nblocks % 8 == 0)
     int nblocks;
+    int dbg;       // diagnostics only (PO2Q_X3_DEBUG): 1 no MFMA, 2 no split, 4 no x loads, 8 no stores
 };
 
 // Exact 3-way bf16 split of 8 fp32 values (bit patterns); non-finite values keep
@@ -80,6 +81,19 @@ __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4&
     lo = make_uint4(l16[0] | (l16[1] << 16), l16[2] | (l16[3] << 16), l16[4] | (l16[5] << 16), l16[6] | (l16[7] << 16));
 }
 
+// Epilogue stores as inline asm: hipcc then leaves them out of its vmcnt
+// bookkeeping.  Loads and stores share vmcnt on gfx950, and the stores of a tile
+// are issued BEFORE the next prefetch, so every compiler wait for the prefetched
+// x also covers these (older) stores; without this hipcc makes the following
+// MFMAs wait for the stores' completion (register reuse WAR).  `s_nop 1` lets
+// the store read its VGPRs before hipcc's next instruction may overwrite them.
+__device__ __forceinline__ void store_f4(float* p, floatx4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_f1(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
 // LDS byte address of channel octet `coct` of halo pixel `hp` inside a plane.
 template <int CC>
 __device__ __forceinline__ int x_addr(int hp, int coct) {
@@ -90,44 +104,146 @@ __device__ __forceinline__ int x_addr(int hp, int coct) {
     }
 }
 
-template <int CC, int NT, int NJ>
-__global__ __launch_bounds__(kThreads) void conv_bf16x3(const float* __restrict__ x, const uint4* __restrict__ wpk,
-                                                        const float* __restrict__ scale_p,
-                                                        const float* __restrict__ bias, float* __restrict__ y,
-                                                        X3Args a) {
+constexpr int kXI = 3;  // max x-staging items (pixel x channel octet) per thread per work item
+constexpr int kWI = 5;  // max weight fragments (uint4) per thread per chunk
+
+// Output tile / image / k-block of virtual tile index v (XCD-aware when T % 8 == 0:
+// the T/8 logical tiles an XCD owns are contiguous, so neighbouring tiles -- which
+// share halo rows -- are processed under the same L2).
+struct TileCoord {
+    int n, kb, p0, q0;
+};
+
+__device__ __forceinline__ TileCoord tile_of(int v, const X3Args& a) {
+    if (a.remap) v = (v & 7) * (a.nblocks >> 3) + (v >> 3);
+    const int tiles = a.tilesP * a.tilesQ;
+    const int tile = v % tiles;
+    v /= tiles;
+    TileCoord t;
+    t.kb = v % a.kblocks;
+    t.n = v / a.kblocks;
+    t.p0 = (tile / a.tilesQ) * a.TP;
+    t.q0 = (tile % a.tilesQ) * a.TQ;
+    return t;
+}
+
+// Persistent, software-pipelined: each block walks work items (tile, chunk) =
+// blockIdx.x + i*gridDim.x tiles x nchunks chunks.  The NEXT item's x halo
+// (fp32, straight to registers) and weight fragments are loaded right after
+// the current item is in LDS, so HBM latency hides behind the MFMA work and
+// the epilogue stores of the current item.
+//   x loads: raw buffer loads, one 32-bit voffset per staged item and the
+//   channel stride in the SGPR soffset (8 loads, zero address VALU); halo
+//   pixels outside the image and channels >= C get an out-of-range offset, so
+//   the hardware bounds check returns the zero padding.
+//   KS > 0: compile-time k-steps per chunk (tap offsets live in registers).
+template <int CC, int NT, int NJ, int KS, bool MC>
+__global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restrict__ x,
+                                                           const uint4* __restrict__ wpk,
+                                                           const float* __restrict__ scale_p,
+                                                           const float* __restrict__ bias, float* __restrict__ y,
+                                                           X3Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int OCT = CC / 8;  // channel octets per tap
+    constexpr int KSR = KS ? KS : 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-    int bid = blockIdx.x;
-    if (a.remap) bid = (bid & 7) * (a.nblocks >> 3) + (bid >> 3);  // same-XCD blocks -> adjacent tiles
-    const int tiles = a.tilesP * a.tilesQ;
-    const int tile = bid % tiles;
-    bid /= tiles;
-    const int kb = bid % a.kblocks;
-    const int n = bid / a.kblocks;
-    const int p0 = (tile / a.tilesQ) * a.TP, q0 = (tile % a.tilesQ) * a.TQ;
-    const int h0 = p0 * a.sh - a.ph, w0 = q0 * a.sw - a.pw;
+    const int T = a.nblocks;     // total tiles (N * kblocks * tilesP * tilesQ)
     const int npix = a.TP * a.TQ;
     const int hw_halo = a.HH * a.WW;
     const int zero_off = hw_halo * (2 * CC);  // 16 zero bytes after the halo pixels of each plane
+    const int items = hw_halo * OCT;
+    const int ksteps = KS ? KS : a.ksteps;
+    const int kfr = ksteps * NT * 64;         // weight fragments (uint4) per chunk
+    const int64_t HWi = (int64_t)a.H * a.W;
+    const uint32_t cstride = (uint32_t)HWi * 4u;  // channel stride, bytes (planner: < 2^28)
+    int v = blockIdx.x;
+    if (v >= T) return;
+    const int o = lane >> 4;
 
     int* tapt = reinterpret_cast<int*>(lds + a.tap_off);
-    if (tid < a.taps) {
+    if (!KS && tid < a.taps) {
         const int r = tid / a.S, s = tid - (tid / a.S) * a.S;
         tapt[tid] = r * a.dh * a.WW + s * a.dw;
     }
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.plane + zero_off) = make_uint4(0u, 0u, 0u, 0u);
 
-    // halo pixel of this lane's pixel in each group (tile-linear, row-major)
-    int hp0[NJ];
+    // halo pixel of this lane's pixel in each group (tile-linear, row-major);
+    // epilogue position of its 4-pixel run
+    int hp0[NJ], ep[NJ];
 #pragma unroll
     for (int g = 0; g < NJ; ++g) {
         int slot = (wave * NJ + g) * 16 + (lane & 15);
         if (slot >= npix) slot = 0;
         const int pl = slot / a.TQ, ql = slot - (slot / a.TQ) * a.TQ;
         hp0[g] = pl * a.sh * a.WW + ql * a.sw;
+        const int i0 = (wave * NJ + g) * 16 + 4 * o;
+        ep[g] = (i0 < npix) ? (((i0 / a.TQ) << 16) | (i0 - (i0 / a.TQ) * a.TQ)) : -1;
     }
+    // per-lane tap offsets for compile-time k-steps: pixel offset, channel octet, pad flag
+    int tpx[KSR], tco[KSR];
+    unsigned padm = 0;
+    if constexpr (KS > 0) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int oi = ks * 4 + o;
+            const int t = oi / OCT;
+            tco[ks] = oi % OCT;
+            const int r = t / a.S, s = t - (t / a.S) * a.S;
+            tpx[ks] = r * a.dh * a.WW + s * a.dw;
+            if (t >= a.taps) padm |= 1u << ks;
+        }
+    }
+    // staging descriptors: this thread's (halo row, halo col, channel octet) per item
+    uint32_t pk[kXI];
+#pragma unroll
+    for (int r = 0; r < kXI; ++r) {
+        const int it = tid + r * kThreads;
+        const int oc = it / hw_halo;
+        const int hp = it - oc * hw_halo;
+        const int hh = hp / a.WW, ww = hp - (hp / a.WW) * a.WW;
+        pk[r] = (it < items) ? (0x80000000u | ((uint32_t)hh << 20) | ((uint32_t)ww << 8) | (uint32_t)oc) : 0u;
+    }
+
+    uint32_t xr[kXI][8];
+    uint4 wr[MC ? kWI : 1];
+
+    auto load_x = [&](const TileCoord& tc, int chunk) {
+        const int h0 = tc.p0 * a.sh - a.ph, w0 = tc.q0 * a.sw - a.pw;
+        const float* base = x + ((int64_t)tc.n * a.C + chunk * CC) * HWi;
+        const int64_t rem = (int64_t)(a.C - chunk * CC) * HWi * 4;
+        const int nrec = (int)(rem > 0x7fffffffLL ? 0x7fffffffLL : rem);
+        const uintptr_t bp = reinterpret_cast<uintptr_t>(base);
+        const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+        const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+        const void* bu = reinterpret_cast<const void*>(((uintptr_t)bhi << 32) | blo);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(bu), (short)0,
+                                                                           __builtin_amdgcn_readfirstlane(nrec),
+                                                                           0x00020000);
+#pragma unroll
+        for (int r = 0; r < kXI; ++r) {
+            const uint32_t d = pk[r];
+            const int hh = (int)((d >> 20) & 0x7ffu), ww = (int)((d >> 8) & 0xfffu), oc = (int)(d & 0xffu);
+            const int h = h0 + hh, w = w0 + ww;
+            const bool ok = (d >> 31) && ((unsigned)h < (unsigned)a.H) && ((unsigned)w < (unsigned)a.W) &&
+                            !(a.dbg & 4);
+            const uint32_t vo = ok ? ((uint32_t)(oc * 8) * cstride + (uint32_t)(h * a.W + w) * 4u) : 0x7fffffffu;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xr[r][j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * cstride, 0);
+        }
+    };
+    auto load_w = [&](int kb, int chunk) {
+        const uint4* wc = wpk + ((int64_t)kb * a.nchunks + chunk) * kfr;
+        if constexpr (MC) {
+#pragma unroll
+            for (int r = 0; r < kWI; ++r) {
+                const int e = tid + r * kThreads;
+                wr[r] = wc[e < kfr ? e : kfr - 1];
+            }
+        } else {  // one (k-block, chunk) for the whole launch: straight to LDS, once
+            uint4* wl0 = reinterpret_cast<uint4*>(lds + a.w_off);
+            for (int e = tid; e < kfr; e += kThreads) wl0[e] = wc[e];
+        }
+    };
 
     floatx4 acc[NJ][NT];
 #pragma unroll
@@ -135,45 +251,129 @@ __global__ __launch_bounds__(kThreads) void conv_bf16x3(const float* __restrict_
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    const int kstep_frags = a.ksteps * NT * 64;  // uint4 per chunk
-    const uint4* wsrc = wpk + (int64_t)kb * a.nchunks * kstep_frags;
+    const float scale = *scale_p;
     uint4* wl = reinterpret_cast<uint4*>(lds + a.w_off);
-    const int64_t HWi = (int64_t)a.H * a.W;
-    const float* ximg = x + (int64_t)n * a.C * HWi;
-    const int o = lane >> 4;
+    const int trash = zero_off + 16;  // per-plane 16-byte slot for padding items
 
-    for (int chunk = 0; chunk < a.nchunks; ++chunk) {
-        const int c0 = chunk * CC;
-        // ---- stage the x halo tile: one (pixel, channel octet) per item, lanes along W
-        const int items = hw_halo * OCT;
-        for (int it = tid; it < items; it += kThreads) {
-            const int oc = it / hw_halo;
-            const int hp = it - oc * hw_halo;
-            const int hh = hp / a.WW, ww = hp - (hp / a.WW) * a.WW;
-            const int h = h0 + hh, w = w0 + ww;
-            const bool v = (h >= 0) && (h < a.H) && (w >= 0) && (w < a.W);
-            const int cb = c0 + oc * 8;
-            const float* src = ximg + (v ? ((int64_t)cb * HWi + (int64_t)h * a.W + w) : 0);
-            uint32_t b[8];
+    // bias through a buffer descriptor: k >= K and bias == nullptr read 0 without a
+    // branch; loaded with the tile's x prefetch so the epilogue issues no loads (a
+    // load there would make every following store wait for all earlier stores)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), (short)0, bias ? a.K * 4 : 0, 0x00020000);
+    float bias_next[NT], bias_done[NT];
+    auto load_bias = [&](int kb) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) b[j] = (v && cb + j < a.C) ? __float_as_uint(src[j * HWi]) : 0u;
+        for (int nt = 0; nt < NT; ++nt)
+            bias_next[nt] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(brs, (uint32_t)(kb * 16 * NT + nt * 16 + (lane & 15)) * 4u, 0, 0));
+    };
+
+    // Epilogue of a finished tile: D[row = pixel 4*(lane>>4)+i][col = channel lane&15]
+    auto epilogue = [&](const TileCoord& tcs) {
+        const int64_t PQ = (int64_t)a.P * a.Q;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int k = tcs.kb * 16 * NT + nt * 16 + (lane & 15);
+            const bool kv = k < a.K;
+            const float bk = bias_done[nt];
+            float* yk = y + ((int64_t)tcs.n * a.K + k) * PQ;
+#pragma unroll
+            for (int g = 0; g < NJ; ++g) {
+                if (a.vec) {
+                    const int pp = tcs.p0 + (ep[g] >> 16), qq = tcs.q0 + (ep[g] & 0xffff);
+                    if (kv && ep[g] >= 0 && pp < a.P && qq < a.Q) {
+                        floatx4 r4;
+                        r4[0] = acc[g][nt][0] * scale + bk;
+                        r4[1] = acc[g][nt][1] * scale + bk;
+                        r4[2] = acc[g][nt][2] * scale + bk;
+                        r4[3] = acc[g][nt][3] * scale + bk;
+                        store_f4(yk + (int64_t)pp * a.Q + qq, r4);
+                    }
+                } else {
+                    const int i0 = (wave * NJ + g) * 16 + 4 * o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int idx = i0 + i;
+                        const int pl = idx / a.TQ, ql = idx - (idx / a.TQ) * a.TQ;
+                        const int pp = tcs.p0 + pl, qq = tcs.q0 + ql;
+                        if (kv && idx < npix && pp < a.P && qq < a.Q)
+                            store_f1(yk + (int64_t)pp * a.Q + qq, acc[g][nt][i] * scale + bk);
+                    }
+                }
+                acc[g][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+
+    TileCoord tc = tile_of(v, a);
+    TileCoord done_tc = tc;  // tile whose finished sums sit in acc (stored one step later)
+    bool done = false;
+    int chunk = 0;
+    load_bias(tc.kb);
+    load_x(tc, 0);
+    load_w(tc.kb, 0);
+    float bias_cur[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bias_cur[nt] = bias_done[nt] = 0.0f;
+
+    // Per work item, in this order (vmcnt counts loads AND stores in issue order, so
+    // the stores of the previous tile go out BEFORE the next prefetch: waiting for the
+    // prefetch at the top of the loop then never waits for just-issued stores):
+    //   barrier | x regs -> split -> LDS, weights -> LDS | barrier |
+    //   stores of the previous tile | prefetch next item | MFMAs of this item
+    while (true) {
+        __syncthreads();  // the previous item's MFMAs are done with LDS
+#pragma unroll
+        for (int r = 0; r < kXI; ++r) {  // unconditional: padding items go to the trash slot
+            const uint32_t d = pk[r];
+            const int hp = (int)((d >> 20) & 0x7ffu) * a.WW + (int)((d >> 8) & 0xfffu);
             uint4 hi, mid, lo;
-            split3(b, hi, mid, lo);
-            const int ad = x_addr<CC>(hp, oc);
+            if (a.dbg & 2) {
+                hi = make_uint4(xr[r][0], xr[r][1], xr[r][2], xr[r][3]);
+                mid = lo = make_uint4(xr[r][4], xr[r][5], xr[r][6], xr[r][7]);
+            } else {
+                split3(xr[r], hi, mid, lo);
+            }
+            const int ad = (d >> 31) ? x_addr<CC>(hp, (int)(d & 0xffu)) : trash;
             *reinterpret_cast<uint4*>(lds + ad) = hi;
             *reinterpret_cast<uint4*>(lds + a.plane + ad) = mid;
             *reinterpret_cast<uint4*>(lds + 2 * a.plane + ad) = lo;
         }
-        // ---- stage this chunk's weight fragments
-        const uint4* wc = wsrc + (int64_t)chunk * kstep_frags;
-        for (int e = tid; e < kstep_frags; e += kThreads) wl[e] = wc[e];
+        if constexpr (MC) {
+#pragma unroll
+            for (int r = 0; r < kWI; ++r) {
+                const int e = tid + r * kThreads;
+                wl[e < kfr ? e : kfr - 1] = wr[r];
+            }
+        }
         __syncthreads();
+        if (chunk == 0) {  // bias of this tile arrived with its first chunk's x
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bias_cur[nt] = bias_next[nt];
+        }
 
-        for (int ks = 0; ks < a.ksteps; ++ks) {
-            const int oi = ks * 4 + o;
-            const int t = oi / OCT, coct = oi % OCT;
-            const bool pad = t >= a.taps;
-            const int toff = pad ? 0 : tapt[t];
+        if (done && !(a.dbg & 8)) {
+            epilogue(done_tc);
+            done = false;
+        }
+
+        // ---- prefetch the next work item, unconditionally (past the end: a harmless
+        // re-load of the current item), so no control-flow join follows the loads
+        int nv = v, nchunk = chunk + 1;
+        if (nchunk == a.nchunks) {
+            nchunk = 0;
+            nv = v + gridDim.x;
+        }
+        const bool more = nv < T;
+        TileCoord ntc = tc;
+        if (nv != v) ntc = tile_of(more ? nv : v, a);
+        const int lchunk = more ? nchunk : chunk;
+        load_bias(ntc.kb);
+        load_x(ntc, lchunk);
+        if constexpr (MC) load_w(ntc.kb, lchunk);
+
+        // ---- MFMAs over this chunk: k = (tap, channel), 32 per step
+        auto kstep = [&](int ks, int toff, int coct, bool pad) {
             bf16x8 bw[NT];
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
@@ -183,7 +383,8 @@ __global__ __launch_bounds__(kThreads) void conv_bf16x3(const float* __restrict_
                 const int ad = pad ? zero_off : x_addr<CC>(hp0[g] + toff, coct);
                 const bf16x8 a0 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + ad));
                 const bf16x8 a1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + a.plane + ad));
-                const bf16x8 a2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + 2 * a.plane + ad));
+                const bf16x8 a2 =
+                    __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + 2 * a.plane + ad));
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     acc[g][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[nt], acc[g][nt], 0, 0, 0);
@@ -191,53 +392,38 @@ __global__ __launch_bounds__(kThreads) void conv_bf16x3(const float* __restrict_
                     acc[g][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bw[nt], acc[g][nt], 0, 0, 0);
                 }
             }
-        }
-        __syncthreads();
-    }
-
-    // ---- epilogue: D[row = pixel 4*(lane>>4)+i][col = channel lane&15]
-    const float scale = *scale_p;
-    const int64_t PQ = (int64_t)a.P * a.Q;
+        };
+        if (a.dbg & 1) {
+        } else if constexpr (KS > 0) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int k = kb * 16 * NT + nt * 16 + (lane & 15);
-        if (k >= a.K) continue;
-        const float bk = bias ? bias[k] : 0.0f;
-        float* yk = y + ((int64_t)n * a.K + k) * PQ;
-#pragma unroll
-        for (int g = 0; g < NJ; ++g) {
-            const int i0 = (wave * NJ + g) * 16 + 4 * (lane >> 4);
-            if (a.vec) {
-                if (i0 >= npix) continue;
-                const int pl = i0 / a.TQ, ql = i0 - (i0 / a.TQ) * a.TQ;
-                const int pp = p0 + pl, qq = q0 + ql;
-                if (pp >= a.P || qq >= a.Q) continue;
-                float4 v;
-                v.x = acc[g][nt][0] * scale + bk;
-                v.y = acc[g][nt][1] * scale + bk;
-                v.z = acc[g][nt][2] * scale + bk;
-                v.w = acc[g][nt][3] * scale + bk;
-                *reinterpret_cast<float4*>(yk + (int64_t)pp * a.Q + qq) = v;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int idx = i0 + i;
-                    if (idx >= npix) continue;
-                    const int pl = idx / a.TQ, ql = idx - (idx / a.TQ) * a.TQ;
-                    const int pp = p0 + pl, qq = q0 + ql;
-                    if (pp >= a.P || qq >= a.Q) continue;
-                    yk[(int64_t)pp * a.Q + qq] = acc[g][nt][i] * scale + bk;
-                }
+            for (int ks = 0; ks < KS; ++ks) kstep(ks, tpx[ks], tco[ks], (padm >> ks) & 1u);
+        } else {
+            for (int ks = 0; ks < ksteps; ++ks) {
+                const int oi = ks * 4 + o;
+                const int t = oi / OCT;
+                const bool pad = t >= a.taps;
+                kstep(ks, pad ? 0 : tapt[t], oi % OCT, pad);
             }
         }
+        if (chunk == a.nchunks - 1) {
+            done = true;
+            done_tc = tc;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bias_done[nt] = bias_cur[nt];
+        }
+        if (!more) break;
+        v = nv;
+        chunk = nchunk;
+        tc = ntc;
     }
+    if (!(a.dbg & 8)) epilogue(done_tc);
 }
 
 // ------------------------------------------------------------------ planning --
 static int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 static size_t x3_lds(const ConvPlan& p, int NT, int HH, int WW) {
-    const int plane = HH * WW * p.SB + 16;
+    const int plane = HH * WW * p.SB + 32;
     return (size_t)3 * plane + (size_t)p.steps * NT * 1024 + 64 * sizeof(int);
 }
 
@@ -248,54 +434,57 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
     if (lo < -126 || hi > 127) return false;  // +-2^e must be a normal bf16
     p.taps = p.R * p.S;
     if (p.taps > 64) return false;
+    if ((int64_t)p.H * p.W * 4 * 32 >= (1LL << 31)) return false;  // 32-bit buffer offsets per chunk
     p.CC = (p.taps == 1 && p.C > 16) ? 32 : 16;
     const int OCT = p.CC / 8;
     p.steps = cdiv(p.taps * OCT, 4);
     p.SB = 2 * p.CC;
     p.NT = p.K <= 16 ? 1 : (p.K <= 32 ? 2 : 4);
+    while (p.NT > 1 && p.steps * p.NT * 64 > kWI * kThreads) p.NT >>= 1;
+    if (p.steps * p.NT * 64 > kWI * kThreads) return false;
     p.kblocks = cdiv(p.K, 16 * p.NT);
     p.nchunks = cdiv(p.C, p.CC);
 
-    // tile search (override: PO2Q_X3_TILE="NJ,TP,TQ", a tuning knob)
+    // tile search (override: PO2Q_X3_TILE="NJ,TP,TQ", a tuning knob; it must pass
+    // the same validity checks as every searched candidate)
     int bestNJ = 0, bestTP = 0, bestTQ = 0;
     double best = 1e300;
-    const char* env = getenv("PO2Q_X3_TILE");
-    if (env) {
-        int nj = 0, tp = 0, tq = 0;
-        if (sscanf(env, "%d,%d,%d", &nj, &tp, &tq) == 3 && tp * tq == 64 * nj &&
-            (nj == 1 || nj == 2 || nj == 4 || nj == 7 || nj == 8)) {
-            bestNJ = nj; bestTP = tp; bestTQ = tq; best = 0;
-        }
-    }
-    const int njs[] = {1, 2, 4, 7, 8};
-    for (int nj : njs) {
-        if (best == 0) break;
-        if (nj * p.NT > 16) continue;
+    auto consider = [&](int nj, int tp, int tq, bool forced) {
+        if (nj == 7 && p.NT > 1) return;  // > 256 VGPRs: spills
+        if (tp < 1 || tq < 1 || tp * tq != 64 * nj) return;
         const int px = 64 * nj;
-        for (int tq = 1; tq <= std::min(p.Q, px); ++tq) {
-            if (px % tq) continue;
-            const int tp = px / tq;
-            const int HH = (tp - 1) * p.sh + (p.R - 1) * p.dh + 1;
-            const int WW = (tq - 1) * p.sw + (p.S - 1) * p.dw + 1;
-            const size_t lds = x3_lds(p, p.NT, HH, WW);
-            if (lds > 64 * 1024) continue;
-            const int tP = cdiv(p.P, tp), tQ = cdiv(p.Q, tq);
-            const double launched = (double)tP * tQ * px;
-            const double waste = launched / ((double)p.P * p.Q);
-            const double halo = (double)tP * tQ * HH * WW / ((double)p.P * p.Q * p.sh * p.sw);
-            const int bpc = std::min<int>(8, (int)((160 * 1024) / lds));
-            const int waves = std::min(bpc * 4, 32);
-            double cost = waste + 0.35 * (halo - 1.0);
-            if (waves < 8) cost += 0.15 * (8 - waves) / 4.0;
-            if (tq % 16 && tq != p.Q) cost += 0.05;
-            if (tq % 4) cost += 0.1;
-            cost += 0.02 * (8.0 / nj);  // per-block fixed costs (barriers, weight staging)
-            const double blocks = (double)p.N * p.kblocks * tP * tQ;
-            if (blocks < 1024) cost += 0.5 * (1024 - blocks) / 1024;
-            if (cost < best) {
-                best = cost; bestNJ = nj; bestTP = tp; bestTQ = tq;
-            }
+        const int HH = (tp - 1) * p.sh + (p.R - 1) * p.dh + 1;
+        const int WW = (tq - 1) * p.sw + (p.S - 1) * p.dw + 1;
+        const size_t lds = x3_lds(p, p.NT, HH, WW);
+        if (lds > 64 * 1024) return;
+        if (HH * WW * (p.CC / 8) > kXI * kThreads) return;  // staged items per thread
+        if (HH >= 2048 || WW >= 4096) return;               // packed staging descriptors
+        const int tP = cdiv(p.P, tp), tQ = cdiv(p.Q, tq);
+        const double launched = (double)tP * tQ * px;
+        const double waste = launched / ((double)p.P * p.Q);
+        const double halo = (double)tP * tQ * HH * WW / ((double)p.P * p.Q * p.sh * p.sw);
+        const int bpc = std::min<int>(8, (int)((160 * 1024) / lds));
+        const int waves = std::min(bpc * 4, 32);
+        double cost = waste + 0.35 * (halo - 1.0);
+        if (waves < 8) cost += 0.15 * (8 - waves) / 4.0;
+        if (tq % 16 && tq != p.Q) cost += 0.05;
+        if (tq % 4) cost += 0.1;
+        cost += 0.02 * (8.0 / nj);  // per-tile fixed costs (barriers, descriptors)
+        const double blocks = (double)p.N * p.kblocks * tP * tQ;
+        if (blocks < 1024) cost += 0.5 * (1024 - blocks) / 1024;
+        if (forced) cost = -1.0;
+        if (cost < best) {
+            best = cost; bestNJ = nj; bestTP = tp; bestTQ = tq;
         }
+    };
+    const char* env = getenv("PO2Q_X3_TILE");
+    int fnj = 0, ftp = 0, ftq = 0;
+    if (env && sscanf(env, "%d,%d,%d", &fnj, &ftp, &ftq) == 3) consider(fnj, ftp, ftq, true);
+    if (best >= 0) {
+        const int njs[] = {1, 2, 4, 7};
+        for (int nj : njs)
+            for (int tq = 1; tq <= std::min(p.Q, 64 * nj); ++tq)
+                if ((64 * nj) % tq == 0) consider(nj, 64 * nj / tq, tq, false);
     }
     if (!bestNJ) return false;
     p.kind = KIND_BF16X3;
@@ -304,7 +493,7 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
     p.tilesQ = cdiv(p.Q, p.TQ);
     p.HH = (p.TP - 1) * p.sh + (p.R - 1) * p.dh + 1;
     p.WW = (p.TQ - 1) * p.sw + (p.S - 1) * p.dw + 1;
-    p.plane = p.HH * p.WW * p.SB + 16;
+    p.plane = p.HH * p.WW * p.SB + 32;  // + zero slot + trash slot
     p.lds_bytes = x3_lds(p, p.NT, p.HH, p.WW);
     p.WWp = p.WW; p.PS = 0; p.MI = 0;
     // packed bf16 fragments: [kb][chunk][ks][nt][lane][8] -> 4-byte words
@@ -314,23 +503,48 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
     return true;
 }
 
-template <int CC, int NT, int NJ>
+template <int CC, int NT, int NJ, int KS, bool MC>
 static hipError_t launch_x3(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
                             const float* scale, const float* bias, float* y, hipStream_t s) {
-    hipLaunchKernelGGL((conv_bf16x3<CC, NT, NJ>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    // persistent grid: as many blocks as can be co-resident (LDS / VGPR occupancy)
+    int per_cu = 0, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_bf16x3<CC, NT, NJ, KS, MC>, kThreads, p.lds_bytes) !=
+            hipSuccess || per_cu < 1)
+        per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    const int64_t grid = std::min<int64_t>(p.blocks, (int64_t)per_cu * cus);
+    hipLaunchKernelGGL((conv_bf16x3<CC, NT, NJ, KS, MC>), dim3((unsigned)grid), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
+}
+
+template <int CC, int NT, int NJ>
+static hipError_t launch_x3_ks(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
+                               const float* scale, const float* bias, float* y, hipStream_t s) {
+    const bool mc = p.nchunks > 1 || p.kblocks > 1;
+    if (p.steps == 1)
+        return mc ? launch_x3<CC, NT, NJ, 1, true>(p, a, x, packed, scale, bias, y, s)
+                  : launch_x3<CC, NT, NJ, 1, false>(p, a, x, packed, scale, bias, y, s);
+    if constexpr (CC == 16)
+        if (p.steps == 5)
+            return mc ? launch_x3<CC, NT, NJ, 5, true>(p, a, x, packed, scale, bias, y, s)
+                      : launch_x3<CC, NT, NJ, 5, false>(p, a, x, packed, scale, bias, y, s);
+    return mc ? launch_x3<CC, NT, NJ, 0, true>(p, a, x, packed, scale, bias, y, s)
+              : launch_x3<CC, NT, NJ, 0, false>(p, a, x, packed, scale, bias, y, s);
 }
 
 template <int CC, int NT>
 static hipError_t launch_x3_nj(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
                                const float* scale, const float* bias, float* y, hipStream_t s) {
     switch (p.NJ) {
-        case 1: return launch_x3<CC, NT, 1>(p, a, x, packed, scale, bias, y, s);
-        case 2: return launch_x3<CC, NT, 2>(p, a, x, packed, scale, bias, y, s);
-        case 4: return launch_x3<CC, NT, 4>(p, a, x, packed, scale, bias, y, s);
-        case 7: return launch_x3<CC, NT, 7>(p, a, x, packed, scale, bias, y, s);
-        default: return launch_x3<CC, NT, 8>(p, a, x, packed, scale, bias, y, s);
+        case 1: return launch_x3_ks<CC, NT, 1>(p, a, x, packed, scale, bias, y, s);
+        case 2: return launch_x3_ks<CC, NT, 2>(p, a, x, packed, scale, bias, y, s);
+        case 4: return launch_x3_ks<CC, NT, 4>(p, a, x, packed, scale, bias, y, s);
+        default:
+            if constexpr (NT == 1) return launch_x3_ks<CC, NT, 7>(p, a, x, packed, scale, bias, y, s);
+            return hipErrorInvalidValue;  // the planner never pairs NJ = 7 with NT > 1 (register file)
     }
 }
 
@@ -357,6 +571,8 @@ hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t*
     a.vec = (p.Q % 4 == 0 && p.TQ % 4 == 0) ? 1 : 0;
     a.nblocks = (int)p.blocks;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
+    const char* dbg = getenv("PO2Q_X3_DEBUG");  // timing diagnostics only: outputs are wrong
+    a.dbg = dbg ? atoi(dbg) : 0;
     if (p.CC == 16) return launch_x3_nt<16>(p, a, x, packed, scale, bias, y, s);
     return launch_x3_nt<32>(p, a, x, packed, scale, bias, y, s);
 }

@@ -1,0 +1,41 @@
+"""Timing ablation of the bf16x3 conv kernel (PO2Q_X3_DEBUG bits: 1 no MFMA,
+2 no split, 4 no x loads, 8 no stores) for one layer shape / tile.  Outputs of
+the ablated runs are meaningless; only their time is.  GPU only."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from po2_quantization_amd import _lib  # noqa: E402
+from tools.tile_sweep import timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="16,224,16,3,1,1")
+    ap.add_argument("--tile", default=None)
+    ap.add_argument("--batch", type=int, default=256)
+    args = ap.parse_args()
+    C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
+    if args.tile:
+        os.environ["PO2Q_X3_TILE"] = args.tile
+    dev = torch.device("cuda:0")
+    x = torch.randn(args.batch, C, H, H, device=dev)
+    w = torch.randn(K, C, R, R, device=dev) * 0.1
+    res = {"plan": _lib.describe(args.batch, C, H, H, K, R, R, st, pad)}
+    for dbg in (0, 1, 2, 3, 4, 8, 12, 5, 7, 9, 11, 13, 14, 15):
+        os.environ["PO2Q_X3_DEBUG"] = str(dbg)
+        res[str(dbg)] = round(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), 7), 4)
+    os.environ.pop("PO2Q_X3_DEBUG")
+    # reference points: torch copy of the same bytes
+    y = torch.empty_like(x)
+    res["copy_in_bytes_ms"] = round(timeit(lambda: y.copy_(x), 7), 4)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,10 @@ for s in $STEPS; do
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
+        pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
+        pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
+        counters) run counters 120 rocprofv3 -L ;;
+        ablate) run ablate 600 bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 --tile 4,8,32 && python tools/ablate.py --shape 64,56,64,3,1,1 --tile 4,8,32 && python tools/ablate.py --shape 32,112,32,3,1,1 --tile 4,16,16' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
                   -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s" ;;

@@ -1,0 +1,39 @@
+"""Run ONE fused quantize+conv layer a few times (for rocprofv3 kernel traces /
+PMC counters).  Shape defaults to ResNet56 stage 1 @224, bs=256.
+
+    python tools/prof_layer.py --shape 16,224,16,3,1,1 --iters 5 [--tile NJ,TP,TQ]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="16,224,16,3,1,1", help="C,H,K,R,stride,pad")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tile", default=None)
+    ap.add_argument("--precision", default="auto")
+    args = ap.parse_args()
+    if args.tile:
+        os.environ["PO2Q_X3_TILE"] = args.tile
+    from po2_quantization_amd import _lib
+
+    C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
+    dev = torch.device("cuda:0")
+    x = torch.randn(args.batch, C, H, H, device=dev)
+    w = torch.randn(K, C, R, R, device=dev) * 0.1
+    print(_lib.describe(args.batch, C, H, H, K, R, R, st, pad, precision=args.precision), flush=True)
+    for _ in range(args.iters):
+        _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", 1, args.precision)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
