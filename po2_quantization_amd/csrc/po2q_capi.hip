@@ -85,7 +85,7 @@ struct WsLayout {
 static WsLayout ws_layout(const ConvPlan& p, int mode) {
     WsLayout L;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    const bool fused = p.kind == KIND_BF16X3 && nw <= kFusedAbsmaxMax;
+    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA) && nw <= kFusedAbsmaxMax;
     L.nparts = (mode == PO2Q_MODE_NONE || fused) ? 0 : absmax_blocks(nw);
     L.part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
     L.scale_off = L.part_bytes;
@@ -138,12 +138,14 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
         st = hip_status(launch_absmax(w, nw, partial, L.nparts, s), "absmax launch");
         if (st) return st;
     }
-    if (p.kind == KIND_BF16X3) {
+    if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA) {
         st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
                                            reinterpret_cast<uint16_t*>(packed), scale, s),
                         "weight pack launch");
         if (st) return st;
-        return hip_status(launch_conv_bf16x3(p, x, reinterpret_cast<const uint16_t*>(packed), scale, bias, y, s),
+        const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
+        return hip_status(p.kind == KIND_BF16X3_DMA ? launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s)
+                                                    : launch_conv_bf16x3(p, x, pk, scale, bias, y, s),
                           "conv launch");
     }
     st = hip_status(launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
@@ -164,12 +166,12 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
     if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
                    flags))
         return PO2Q_ERR_INVALID;
-    static const char* kinds[] = {"mfma_f32", "depthwise", "bf16x3"};
+    static const char* kinds[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma"};
     snprintf(buf, len,
-             "kind=%s CC=%d NT=%d MI=%d NJ=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
-             "lds=%zu blocks=%lld",
-             kinds[p.kind], p.CC, p.NT, p.MI, p.NJ, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW, p.nchunks, p.kblocks,
-             p.steps, p.lds_bytes, (long long)p.blocks);
+             "kind=%s CC=%d NT=%d MI=%d NJ=%d vr=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
+             "lds=%zu blocks=%lld waves=%d",
+             kinds[p.kind], p.CC, p.NT, p.MI, p.NJ, p.vrx, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW, p.nchunks, p.kblocks,
+             p.steps, p.lds_bytes, (long long)p.blocks, p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4);
     return PO2Q_OK;
 }
 

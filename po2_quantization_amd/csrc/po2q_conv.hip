@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "po2q_internal.h"
 
@@ -209,10 +210,18 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
     p.sh = (int)sh; p.sw = (int)sw; p.ph = (int)ph; p.pw = (int)pw; p.dh = (int)dh; p.dw = (int)dw;
     p.groups = (int)groups; p.P = (int)P; p.Q = (int)Q; p.Cg = (int)(C / groups); p.Kg = (int)(K / groups);
 
-    p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S;
+    p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S; p.vrx = 0;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0;
     // bf16x3 split-exact MFMA (po2q_conv_x3.hip): default for quantized weights
     if (flags == 2 || (flags == 0 && mode != 0 && !(p.Cg == 1 && groups > 1))) {
-        if (plan_bf16x3(p, mode, bits, fsr)) return true;
+        if (plan_bf16x3(p, mode, bits, fsr)) {
+            const char* nd = getenv("PO2Q_NO_DMA");  // A/B knob: keep the register-staged kernel
+            if (!(nd && nd[0] == '1')) {
+                ConvPlan q = p;
+                if (plan_bf16x3_dma(q)) p = q;
+            }
+            return true;
+        }
         if (flags == 2) {
             set_error("po2q: bf16x3 precision needs power-of-two weights (mode po2/po2+, exponents within the "
                       "bf16 range) and groups == 1");

@@ -39,11 +39,10 @@
 #include <cstdlib>
 
 #include "po2q_internal.h"
+#include "po2q_x3_dev.h"
 
 namespace po2q {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct X3Args {
     int N, C, H, W, K, P, Q, sh, sw, ph, pw, dh, dw, R, S;
@@ -57,75 +56,8 @@ struct X3Args {
     int dbg;       // diagnostics only (PO2Q_X3_DEBUG): 1 no MFMA, 2 no split, 4 no x loads, 8 no stores
 };
 
-// Exact 3-way bf16 split of 8 fp32 values (bit patterns); non-finite values keep
-// their class in hi (NaN stays NaN) with mid = lo = 0.
-__device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
-    uint32_t h16[8], m16[8], l16[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const uint32_t u = b[j];
-        const bool nonfinite = (u & 0x7f800000u) == 0x7f800000u;
-        const bool nan = nonfinite && (u & 0x007fffffu);
-        const uint32_t hb = u & 0xffff0000u;
-        float r1 = __uint_as_float(u) - __uint_as_float(hb);
-        r1 = nonfinite ? 0.0f : r1;
-        const uint32_t r1b = __float_as_uint(r1);
-        const uint32_t mb = r1b & 0xffff0000u;
-        const float r2 = r1 - __uint_as_float(mb);
-        h16[j] = (hb >> 16) | (nan ? 0x40u : 0u);
-        m16[j] = mb >> 16;
-        l16[j] = __float_as_uint(r2) >> 16;
-    }
-    hi = make_uint4(h16[0] | (h16[1] << 16), h16[2] | (h16[3] << 16), h16[4] | (h16[5] << 16), h16[6] | (h16[7] << 16));
-    mid = make_uint4(m16[0] | (m16[1] << 16), m16[2] | (m16[3] << 16), m16[4] | (m16[5] << 16), m16[6] | (m16[7] << 16));
-    lo = make_uint4(l16[0] | (l16[1] << 16), l16[2] | (l16[3] << 16), l16[4] | (l16[5] << 16), l16[6] | (l16[7] << 16));
-}
-
-// Epilogue stores as inline asm: hipcc then leaves them out of its vmcnt
-// bookkeeping.  Loads and stores share vmcnt on gfx950, and the stores of a tile
-// are issued BEFORE the next prefetch, so every compiler wait for the prefetched
-// x also covers these (older) stores; without this hipcc makes the following
-// MFMAs wait for the stores' completion (register reuse WAR).  `s_nop 1` lets
-// the store read its VGPRs before hipcc's next instruction may overwrite them.
-__device__ __forceinline__ void store_f4(float* p, floatx4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_f1(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-// LDS byte address of channel octet `coct` of halo pixel `hp` inside a plane.
-template <int CC>
-__device__ __forceinline__ int x_addr(int hp, int coct) {
-    if constexpr (CC == 16) {
-        return hp * 32 + coct * 16;
-    } else {
-        return hp * (2 * CC) + ((coct ^ ((hp >> 1) & 3)) << 4);
-    }
-}
-
 constexpr int kXI = 3;  // max x-staging items (pixel x channel octet) per thread per work item
 constexpr int kWI = 5;  // max weight fragments (uint4) per thread per chunk
-
-// Output tile / image / k-block of virtual tile index v (XCD-aware when T % 8 == 0:
-// the T/8 logical tiles an XCD owns are contiguous, so neighbouring tiles -- which
-// share halo rows -- are processed under the same L2).
-struct TileCoord {
-    int n, kb, p0, q0;
-};
-
-__device__ __forceinline__ TileCoord tile_of(int v, const X3Args& a) {
-    if (a.remap) v = (v & 7) * (a.nblocks >> 3) + (v >> 3);
-    const int tiles = a.tilesP * a.tilesQ;
-    const int tile = v % tiles;
-    v /= tiles;
-    TileCoord t;
-    t.kb = v % a.kblocks;
-    t.n = v / a.kblocks;
-    t.p0 = (tile / a.tilesQ) * a.TP;
-    t.q0 = (tile % a.tilesQ) * a.TQ;
-    return t;
-}
 
 // Persistent, software-pipelined: each block walks work items (tile, chunk) =
 // blockIdx.x + i*gridDim.x tiles x nchunks chunks.  The NEXT item's x halo
@@ -488,7 +420,7 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
     }
     if (!bestNJ) return false;
     p.kind = KIND_BF16X3;
-    p.NJ = bestNJ; p.TP = bestTP; p.TQ = bestTQ;
+    p.NJ = bestNJ; p.TP = bestTP; p.TQ = bestTQ; p.vrx = 0;
     p.tilesP = cdiv(p.P, p.TP);
     p.tilesQ = cdiv(p.Q, p.TQ);
     p.HH = (p.TP - 1) * p.sh + (p.R - 1) * p.dh + 1;

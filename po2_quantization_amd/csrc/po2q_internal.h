@@ -26,7 +26,7 @@ hipError_t launch_quantize_plain(const float* w, int64_t n, const unsigned* part
                                  int bits, int fsr, int mode, float* out, hipStream_t s);
 
 // Conv kinds
-enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2 };
+enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2, KIND_BF16X3_DMA = 3 };
 
 // Conv geometry and tiling plan (host-side, shared by workspace sizing and launch).
 struct ConvPlan {
@@ -44,6 +44,9 @@ struct ConvPlan {
     int SB;                      // bf16x3: LDS bytes per halo pixel (per split plane)
     int plane;                   // bf16x3: bytes per split plane (halo + 16 B zero pad)
     int taps;                    // R*S
+    int vrx;                     // bf16x3: row-reuse schedule, waves across (0 = generic k-step schedule)
+    int dma_d0, dma_nck, dma_ni, dma_nw;  // bf16x3 DMA: window offset, 16-B chunks per halo row, DMAs per wave
+    int dma_waves;                // bf16x3 DMA: waves per block (4 or 8)
     int64_t packed_floats;       // packed weight buffer (4-byte words)
     size_t lds_bytes;
     int64_t blocks;
@@ -56,6 +59,10 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
 // bf16x3 planner (po2q_conv_x3.hip): fills the bf16x3 fields of an already
 // validated plan; false if the shape / exponent range is not eligible.
 bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr);
+
+// LDS-DMA pipelined bf16x3 plan (po2q_conv_x3p.hip): refines a bf16x3 plan; false if
+// the shape is not eligible (the po2q_conv_x3.hip plan is then kept).
+bool plan_bf16x3_dma(ConvPlan& p);
 
 // Pack (and quantize unless mode == 0) the weight into the plan's layout.
 hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned* partial, int nparts,
@@ -72,5 +79,8 @@ hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, c
 
 hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t* packed,
                               const float* scale, const float* bias, float* y, hipStream_t s);
+
+hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
+                                  const float* scale, const float* bias, float* y, hipStream_t s);
 
 }  // namespace po2q

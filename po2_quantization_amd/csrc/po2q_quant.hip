@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void pack_mfma_f32_kernel(const float* __
 // scale is not a positive finite number (all-zero / NaN / inf weights) the
 // reference's Q(w) itself (NaN / inf / 0) is stored and the multiplier is 1.
 struct PackX3 {
-    int C, K, R, S, CC, NT, nchunks, ksteps, taps;
+    int C, K, R, S, CC, NT, nchunks, ksteps, taps, vr;
     int64_t total;  // uint16 elements
 };
 
@@ -148,6 +148,17 @@ __device__ __forceinline__ uint16_t bf16_bits_keep_nan(float q) {
     const uint32_t u = __float_as_uint(q);
     const bool nan = ((u & 0x7f800000u) == 0x7f800000u) && (u & 0x007fffffu);
     return (uint16_t)((u >> 16) | (nan ? 0x40u : 0u));
+}
+
+// W' = Q(w) / scale as bf16 bits: sign(w) * 2^e exactly (fin), else the reference's Q(w).
+__device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, int mode, int lo, int hi) {
+    if (fin) {
+        int e = 0;
+        exponent_of(wv, scale, mode, lo, hi, e);  // finite: a = |w/scale| <= 1
+        const float sg = ref_sign(wv);
+        return (sg == 0.0f) ? (uint16_t)0 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
+    }
+    return bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
 }
 
 __global__ __launch_bounds__(kThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
@@ -185,6 +196,24 @@ __global__ __launch_bounds__(kThreads) void pack_bf16x3_kernel(const float* __re
         int64_t t = j;
         const int e8 = (int)(t & 7); t >>= 3;
         const int lane = (int)(t & 63); t >>= 6;
+        if (pg.vr) {
+            // row-reuse layout [chunk][r][f][lane][8], 3x3 / 16 output channels (po2q_conv_x3.hip):
+            //   f = s in 0..2: B[k][n] = w[n][c][r][s] for both k halves (hi|mid A fragment)
+            //   f = 3: k < 16 -> s = 0, k >= 16 -> s = 1;  f = 4: k < 16 -> s = 2, k >= 16 -> 0
+            const int fr = (int)(t % 15);
+            const int chunk = (int)(t / 15);
+            const int r = fr / 5, ft = fr % 5, grp = lane >> 4;
+            const int sft = ft < 3 ? ft : (ft == 3 ? (grp >= 2 ? 1 : 0) : (grp >= 2 ? -1 : 2));
+            const int k = lane & 15;
+            const int c = chunk * 16 + 8 * (grp & 1) + e8;
+            uint16_t v = 0;
+            if (k < pg.K && c < pg.C && sft >= 0) {
+                const float wv = w[(((int64_t)k * pg.C + c) * 3 + r) * 3 + sft];
+                v = pack_one(wv, scale, fin, mode, lo, hi);
+            }
+            packed[j] = v;
+            continue;
+        }
         const int nt = (int)(t % pg.NT); t /= pg.NT;
         const int ks = (int)(t % pg.ksteps); t /= pg.ksteps;
         const int chunk = (int)(t % pg.nchunks);
@@ -197,15 +226,7 @@ __global__ __launch_bounds__(kThreads) void pack_bf16x3_kernel(const float* __re
         if (k < pg.K && c < pg.C && tap < pg.taps) {
             const int r = tap / pg.S, s = tap - (tap / pg.S) * pg.S;
             const float wv = w[(((int64_t)k * pg.C + c) * pg.R + r) * pg.S + s];
-            if (fin) {
-                int e = 0;
-                exponent_of(wv, scale, mode, lo, hi, e);  // finite: a = |w/scale| <= 1
-                const float sg = ref_sign(wv);
-                v = (sg == 0.0f) ? (uint16_t)0
-                                 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
-            } else {
-                v = bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
-            }
+            v = pack_one(wv, scale, fin, mode, lo, hi);
         }
         packed[j] = v;
     }
@@ -217,7 +238,7 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
     clamp_window(bits, fsr, lo, hi);
     PackX3 pg;
     pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
-    pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps;
+    pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps; pg.vr = p.vrx ? 1 : 0;
     pg.total = p.packed_floats * 2;
     int64_t b = (pg.total + 2047) / 2048;
     if (b < 1) b = 1;
@@ -232,7 +253,7 @@ hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned
                                int fsr, int mode, float* packed, hipStream_t s) {
     int lo = 0, hi = 0;
     if (mode != 0) clamp_window(bits, fsr, lo, hi);
-    if (p.kind == 1) {  // depthwise: plain [K][1][R][S] quantized copy
+    if (p.kind == KIND_DEPTHWISE) {  // depthwise: plain [K][1][R][S] quantized copy
         const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
         if (mode == 0) return hipMemcpyAsync(packed, w, n * sizeof(float), hipMemcpyDeviceToDevice, s);
         hipLaunchKernelGGL(quantize_plain_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, w, n, partial, nparts,

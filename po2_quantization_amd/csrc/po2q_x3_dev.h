@@ -1,0 +1,88 @@
+// Device helpers shared by the bf16x3 conv kernels (po2q_conv_x3.hip,
+// po2q_conv_x3p.hip): exact 3-way bf16 split, LDS plane addressing, asm
+// epilogue stores, tile decoding.  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace po2q {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Exact 3-way bf16 split of 8 fp32 values (bit patterns):
+//   hi = x & 0xffff0000, r1 = x - hi (exact), mid = r1 & 0xffff0000, lo = r1 - mid.
+// NaN needs no care (r1 = NaN, so mid/lo are NaN and so is every product sum).
+// +-inf would give r1 = inf - inf = NaN where the reference's product is +-inf, so
+// r1 is forced to 0 there (v_cmp_class + v_cndmask: branch-free, no exec juggling).
+__device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
+    uint32_t mb[8], lb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float xv = __uint_as_float(b[j]);
+        float r1 = xv - __uint_as_float(b[j] & 0xffff0000u);
+        r1 = __builtin_isinf(xv) ? 0.0f : r1;
+        mb[j] = __float_as_uint(r1) & 0xffff0000u;
+        lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
+    }
+    hi = make_uint4((b[0] >> 16) | (b[1] & 0xffff0000u), (b[2] >> 16) | (b[3] & 0xffff0000u),
+                    (b[4] >> 16) | (b[5] & 0xffff0000u), (b[6] >> 16) | (b[7] & 0xffff0000u));
+    mid = make_uint4((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3], (mb[4] >> 16) | mb[5], (mb[6] >> 16) | mb[7]);
+    lo = make_uint4((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u),
+                    (lb[4] >> 16) | (lb[5] & 0xffff0000u), (lb[6] >> 16) | (lb[7] & 0xffff0000u));
+}
+
+// Epilogue stores as inline asm: hipcc then leaves them out of its vmcnt
+// bookkeeping.  Loads and stores share vmcnt on gfx950, and the stores of a tile
+// are issued BEFORE the next prefetch, so every compiler wait for the prefetched
+// x also covers these (older) stores; without this hipcc makes the following
+// MFMAs wait for the stores' completion (register reuse WAR).  `s_nop 1` lets
+// the store read its VGPRs before hipcc's next instruction may overwrite them.
+__device__ __forceinline__ void store_f4(float* p, floatx4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_f1(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+// LDS byte address of channel octet `coct` of halo pixel `hp` inside a plane.
+template <int CC>
+__device__ __forceinline__ int x_addr(int hp, int coct) {
+    if constexpr (CC == 16) {
+        return hp * 32 + coct * 16;
+    } else {
+        return hp * (2 * CC) + ((coct ^ ((hp >> 1) & 3)) << 4);
+    }
+}
+
+// Output tile / image / k-block of virtual tile index v (XCD-aware when T % 8 == 0:
+// the T/8 logical tiles an XCD owns are contiguous, so neighbouring tiles -- which
+// share halo rows -- are processed under the same L2).
+struct TileCoord {
+    int n, kb, p0, q0;
+};
+
+template <class Args>
+__device__ __forceinline__ TileCoord tile_of(int v, const Args& a) {
+    if (a.remap) v = (v & 7) * (a.nblocks >> 3) + (v >> 3);
+    const int tiles = a.tilesP * a.tilesQ;
+    const int tile = v % tiles;
+    v /= tiles;
+    TileCoord t;
+    t.kb = v % a.kblocks;
+    t.n = v / a.kblocks;
+    t.p0 = (tile / a.tilesQ) * a.TP;
+    t.q0 = (tile % a.tilesQ) * a.TQ;
+    return t;
+}
+
+// Division of a wave-uniform 0 <= x < 2^20 by 1 <= d < 2^20 through the host magic
+// number m = floor(2^40 / d) + 1 (< 2^41, passed as lo / hi words): q = (x * m) >> 40,
+// exact in that range (m*d - 2^40 <= d), three SALU ops instead of a ~30-instruction
+// software division (the planner checks the ranges).
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t x, uint32_t mlo, uint32_t mhi) {
+    return (__umulhi(x, mlo) + x * mhi) >> 8;
+}
+
+}  // namespace po2q

@@ -26,14 +26,20 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -x
+               if ! grep -q " passed" gpurun_out/pytest_gpu.log || grep -q "failed\|error" gpurun_out/pytest_gpu.log; then
+                   echo "stopping: GPU tests did not pass"; exit 1
+               fi ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
         counters) run counters 120 rocprofv3 -L ;;
-        ablate) run ablate 600 bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 --tile 4,8,32 && python tools/ablate.py --shape 64,56,64,3,1,1 --tile 4,8,32 && python tools/ablate.py --shape 32,112,32,3,1,1 --tile 4,16,16' ;;
+        stamps) run stamps 600 python tools/stamps.py ;;
+        pmcd1) run pmcd1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" d1 ;;
+        pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;
+        ablate) run ablate 600 bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
                   -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s" ;;

@@ -46,6 +46,23 @@ def main():
         plan = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
         t_auto = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
         res = []
+        # LDS-DMA kernel (po2q_conv_x3p.hip): 4 or 8 waves, tile = 16 * waves * NJ pixels
+        for waves in (4, 8):
+            os.environ["PO2Q_X3P_WAVES"] = str(waves)
+            for nj in (1, 2, 4):
+                px = 16 * waves * nj
+                cands = [(px // tq, tq, 0) for tq in (4, 8, 16, 32, 64, 128) if px % tq == 0]
+                cands += [(nj * (waves // vrx), 16 * vrx, vrx) for vrx in (1, 2, 4, 8) if vrx <= waves]
+                for tp, tq, vrx in cands:
+                    os.environ["PO2Q_X3P_TILE"] = "%d,%d,%d,%d" % (nj, tp, tq, vrx)
+                    d = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
+                    if "bf16x3_dma" not in d or "tile=%dx%d" % (tp, tq) not in d or ("vr=%d" % vrx) not in d:
+                        continue
+                    t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
+                    res.append((t, "dma%d%s" % (waves, "vr%d" % vrx if vrx else ""), nj, tp, tq))
+        os.environ.pop("PO2Q_X3P_TILE", None)
+        os.environ.pop("PO2Q_X3P_WAVES", None)
+        os.environ["PO2Q_NO_DMA"] = "1"
         for nj in (1, 2, 4, 7):
             px = 64 * nj
             for tq in sorted({8, 16, 32, 56, 64, 112, P, 4}):
@@ -59,15 +76,16 @@ def main():
                     t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
                 except RuntimeError as e:
                     continue
-                res.append((t, nj, px // tq, tq))
+                res.append((t, "reg", nj, px // tq, tq))
         os.environ.pop("PO2Q_X3_TILE", None)
-        res.sort()
+        os.environ.pop("PO2Q_NO_DMA", None)
+        res.sort(key=lambda r: r[0])
         flops = 2.0 * args.batch * K * P * P * C * R * R
         nbytes = 4.0 * (args.batch * C * H * H + args.batch * K * P * P + K * C * R * R)
         print(json.dumps({"shape": [C, H, K, R, st], "auto_plan": plan, "auto_ms": round(t_auto, 4),
                           "auto_GBs": round(nbytes / t_auto / 1e6, 1),
                           "auto_TFs": round(flops / t_auto / 1e9, 1),
-                          "best": [(round(t, 4), nj, tp, tq) for t, nj, tp, tq in res[:6]]}), flush=True)
+                          "best": [(round(r[0], 4),) + tuple(r[1:]) for r in res[:8]]}), flush=True)
         del x, w
 
 
