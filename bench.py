@@ -3,9 +3,12 @@
 One step = one pass of the hot path over one batch: the 56 QuantizedConv2d
 layers of ResNet56 in graph order (each a fused PO2 quantize + conv, i.e. the
 reference's QuantizedConv2d.forward, models/quantized_conv.py:32-38), fed by
-the previous layer's output, then the classifier head (global avg-pool + fc)
-and, for N > 1, an RCCL all_gather of the logits over xGMI.  Inputs and
-weights are synthetic (seeded) and resident in HBM before the timed region.
+the previous layer's output, then the classifier head (global avg-pool + fc).
+For N > 1 every rank runs its own batch shard (data-parallel inference: the
+path has no exchange step, so no collective in the timed region; only the
+barrier + max-over-ranks timing).  Inputs and weights are synthetic (seeded)
+and resident in HBM before the timed region.  Each conv shape is autotuned
+on its first (untimed, warmup) call, as the reference's cudnn.benchmark does.
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
@@ -162,7 +165,12 @@ def main():
     ap.add_argument("--precision", default="auto", choices=["auto", "fp32", "bf16x3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="use the heuristic plans instead of autotuning each conv shape on first use")
     args = ap.parse_args()
+    # the reference runs with torch.backends.cudnn.benchmark = True (train.py:33, test.py:31);
+    # the po2q counterpart times every candidate plan on a shape's first call (an untimed warmup step)
+    _lib.benchmark = not args.no_autotune
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -179,16 +187,12 @@ def main():
     chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
     B, Hs = args.batch, args.image
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
-    gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
 
     def step(record=False):
-        logits = chain.forward(x, record)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, logits)
-        return logits
+        return chain.forward(x, record)
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for _ in range(max(args.warmup, 1 if _lib.benchmark else 0)):  # autotuning needs one untimed pass
             step()
         torch.cuda.synchronize()
         if world > 1:
@@ -248,9 +252,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
-        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s"
-                               % (args.model, len(chain.layers), args.quantizer, args.bits,
-                                  " + RCCL all_gather(logits)" if world > 1 else ""),
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head"
+                               % (args.model, len(chain.layers), args.quantizer, args.bits),
+                   "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
                    "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world},
         "roofline": roof,

@@ -67,7 +67,8 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
  * x [N, C, H, W], w [K, C/groups, R, S], bias [K] or NULL, y [N, K, P, Q] with
  * P = (H + 2*pad_h - dil_h*(R-1) - 1)/stride_h + 1 (likewise Q).
  * flags: one of enum po2q_precision.  The workspace size depends on every
- * argument of po2q_qconv2d_workspace_bytes (the plan is chosen from them).
+ * argument of po2q_qconv2d_workspace_bytes (the plan is chosen from them); it
+ * covers every plan po2q_qconv2d_autotune may select.
  */
 size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W,
                                     int64_t K, int64_t R, int64_t S,
@@ -81,6 +82,43 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
                      int64_t dil_h, int64_t dil_w, int64_t groups,
                      int bits, int fsr, int mode, int flags,
                      void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Kernel autotuning, the counterpart of the reference's
+ * torch.backends.cudnn.benchmark = True (train.py:33, test.py:31): times every
+ * candidate plan for this problem on these buffers (synchronises the stream;
+ * not allowed during graph capture), remembers the fastest for the process,
+ * and leaves y = the chosen plan's result.  Later po2q_qconv2d_f32 /
+ * po2q_qconv2d_describe calls with the same arguments use the tuned plan.
+ * buf (may be NULL) receives the chosen plan's description.
+ */
+int po2q_qconv2d_autotune(const float* x, const float* w, const float* bias, float* y,
+                          int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t K, int64_t R, int64_t S,
+                          int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                          int64_t dil_h, int64_t dil_w, int64_t groups,
+                          int bits, int fsr, int mode, int flags,
+                          void* workspace, size_t workspace_bytes, void* stream,
+                          char* buf, size_t len);
+
+/*
+ * Plan enumeration (the counterpart of cuDNN's algorithm enumeration): returns
+ * the number of candidate plans po2q_qconv2d_autotune times for these arguments
+ * (>= 1; plan 0 is the heuristic default), or -status on invalid arguments, and
+ * writes plan `index`'s description to buf when 0 <= index < count.
+ * po2q_qconv2d_f32_plan runs candidate `index` (same contract as po2q_qconv2d_f32).
+ */
+int po2q_qconv2d_plans(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                       int64_t dil_h, int64_t dil_w, int64_t groups,
+                       int bits, int fsr, int mode, int flags, int index, char* buf, size_t len);
+int po2q_qconv2d_f32_plan(int index, const float* x, const float* w, const float* bias, float* y,
+                          int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t K, int64_t R, int64_t S,
+                          int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                          int64_t dil_h, int64_t dil_w, int64_t groups,
+                          int bits, int fsr, int mode, int flags,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /*
  * Diagnostic: the plan po2q_qconv2d_f32 would run for these arguments, as a

@@ -25,8 +25,17 @@ EXPORTS = (
     "po2q_quantize_f32",
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
+    "po2q_qconv2d_autotune",
+    "po2q_qconv2d_plans",
+    "po2q_qconv2d_f32_plan",
     "po2q_qconv2d_describe",
 )
+
+# Kernel autotuning on the first call per conv problem, the counterpart of
+# torch.backends.cudnn.benchmark (reference train.py:33 / test.py:31 set it):
+# None follows torch.backends.cudnn.benchmark, True / False force it.
+benchmark = None
+_tuned = set()
 
 _lib = None
 
@@ -59,6 +68,13 @@ def load():
     L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32, i32, i32]
     L.po2q_qconv2d_f32.restype = i32
     L.po2q_qconv2d_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+    L.po2q_qconv2d_autotune.restype = i32
+    L.po2q_qconv2d_autotune.argtypes = ([p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+                                        + [ctypes.c_char_p, sz])
+    L.po2q_qconv2d_plans.restype = i32
+    L.po2q_qconv2d_plans.argtypes = [i64] * 14 + [i32] * 5 + [ctypes.c_char_p, sz]
+    L.po2q_qconv2d_f32_plan.restype = i32
+    L.po2q_qconv2d_f32_plan.argtypes = [i32, p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
     L.po2q_qconv2d_describe.restype = i32
     L.po2q_qconv2d_describe.argtypes = [i64] * 14 + [i32, i32, i32, i32, ctypes.c_char_p, sz]
     _lib = L
@@ -110,8 +126,11 @@ def _pair(v):
 
 
 def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
-            precision="auto"):
-    """Fused quantize + conv forward (models/quantized_conv.py:32-38); NCHW fp32 in/out."""
+            precision="auto", plan=None):
+    """Fused quantize + conv forward (models/quantized_conv.py:32-38); NCHW fp32 in/out.
+
+    plan=None runs the tuned (or heuristic) plan, autotuning first when benchmark
+    mode is on; plan=i runs candidate i of plans() (tests / tuning tools)."""
     _require_hip_f32(x, "input")
     _require_hip_f32(w, "weight")
     if bias is not None:
@@ -143,10 +162,44 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
             _check(1)
         y = torch.empty((N, K, max(P, 0), max(Q, 0)), dtype=torch.float32, device=xc.device)
         ws = _workspace(nbytes, xc.device)
-        _check(L.po2q_qconv2d_f32(xc.data_ptr(), wc.data_ptr(), bc.data_ptr() if bc is not None else None,
-                                  y.data_ptr(), *args, int(bits), int(fsr), mode_id, prec,
-                                  ws.data_ptr(), ws.numel(), _stream(xc.device)))
+        bp = bc.data_ptr() if bc is not None else None
+        key = args + (int(bits), int(fsr), mode_id, prec)
+        if plan is not None:
+            _check(L.po2q_qconv2d_f32_plan(int(plan), xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
+                                           ws.data_ptr(), ws.numel(), _stream(xc.device)))
+        elif key not in _tuned and _benchmark_enabled():
+            _check(L.po2q_qconv2d_autotune(xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
+                                           ws.data_ptr(), ws.numel(), _stream(xc.device), None, 0))
+            _tuned.add(key)
+        else:
+            _check(L.po2q_qconv2d_f32(xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
+                                      ws.data_ptr(), ws.numel(), _stream(xc.device)))
     return y
+
+
+def _benchmark_enabled():
+    on = torch.backends.cudnn.benchmark if benchmark is None else benchmark
+    return bool(on) and not torch.cuda.is_current_stream_capturing()
+
+
+def plans(N, C, H, W, K, R, S, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+          precision="auto"):
+    """Descriptions of the candidate plans autotuning chooses from (index 0 = heuristic default)."""
+    L = load()
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    dh, dw = _pair(dilation)
+    args = (N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, int(groups), int(bits), int(fsr), MODES[mode],
+            PRECISIONS[precision])
+    n = L.po2q_qconv2d_plans(*args, -1, None, 0)
+    if n < 0:
+        _check(-n)
+    out = []
+    for i in range(n):
+        buf = ctypes.create_string_buffer(512)
+        L.po2q_qconv2d_plans(*args, i, buf, 512)
+        out.append(buf.value.decode())
+    return out
 
 
 def describe(N, C, H, W, K, R, S, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,

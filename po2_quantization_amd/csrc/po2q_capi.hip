@@ -4,8 +4,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/po2q.h"
 #include "po2q_internal.h"
@@ -98,17 +100,23 @@ size_t po2q_qconv2d_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, 
                                        int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
                                        int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode,
                                        int flags) {
+    // the maximum over every plan the autotuner may pick, so one workspace serves
+    // the heuristic plan, the autotune sweep and the tuned plan alike
+    std::vector<ConvPlan> cands;
+    if (!plan_candidates(cands, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags))
+        return 0;
     ConvPlan p;
     if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
                    flags))
         return 0;
-    return ws_layout(p, mode).total;
+    size_t total = ws_layout(p, mode).total;
+    for (const ConvPlan& c : cands) total = std::max(total, ws_layout(c, mode).total);
+    return total;
 }
 
-int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
-                     int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
-                     int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode,
-                     int flags, void* workspace, size_t workspace_bytes, void* stream) {
+static int check_conv_args(const float* x, const float* w, float* y, void* workspace, int mode, int bits,
+                           int flags) {
     if (!check_mode_bits(mode, bits, true)) return PO2Q_ERR_INVALID;
     if (flags < PO2Q_PREC_AUTO || flags > PO2Q_PREC_BF16X3) {
         set_error("po2q: unknown precision flag " + std::to_string(flags));
@@ -118,16 +126,17 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
         set_error("po2q: null pointer");
         return PO2Q_ERR_INVALID;
     }
-    ConvPlan p;
-    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
-                   flags))
-        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    return PO2Q_OK;
+}
+
+// Enqueue the fused quantize(+pack) and conv of plan p on stream s.
+static int run_plan(const ConvPlan& p, const float* x, const float* w, const float* bias, float* y, int bits, int fsr,
+                    int mode, void* workspace, size_t workspace_bytes, hipStream_t s) {
     const WsLayout L = ws_layout(p, mode);
     if (workspace_bytes < L.total) {
         set_error("po2q: conv workspace too small (need " + std::to_string(L.total) + " bytes)");
         return PO2Q_ERR_WORKSPACE;
     }
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     char* ws = reinterpret_cast<char*>(workspace);
     unsigned* partial = reinterpret_cast<unsigned*>(ws);
     float* scale = reinterpret_cast<float*>(ws + L.scale_off);
@@ -154,6 +163,120 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
     return hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
 }
 
+static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma"};
+
+static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
+    snprintf(buf, len,
+             "kind=%s CC=%d NT=%d MI=%d NJ=%d vr=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
+             "lds=%zu blocks=%lld waves=%d",
+             kKindNames[p.kind], p.CC, p.NT, p.MI, p.NJ, p.vrx, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW,
+             p.nchunks, p.kblocks, p.steps, p.lds_bytes, (long long)p.blocks,
+             p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4);
+}
+
+int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
+                     int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
+                     int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode,
+                     int flags, void* workspace, size_t workspace_bytes, void* stream) {
+    int st = check_conv_args(x, w, y, workspace, mode, bits, flags);
+    if (st) return st;
+    ConvPlan p;
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
+                   flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    return run_plan(p, x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
+int po2q_qconv2d_autotune(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
+                          int64_t H, int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w,
+                          int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits,
+                          int fsr, int mode, int flags, void* workspace, size_t workspace_bytes, void* stream,
+                          char* buf, size_t len) {
+    int st = check_conv_args(x, w, y, workspace, mode, bits, flags);
+    if (st) return st;
+    std::vector<ConvPlan> cands;
+    if (!plan_candidates(cands, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    st = hip_status(hipStreamIsCapturing(s, &cs), "stream capture query");
+    if (st) return st;
+    if (cs != hipStreamCaptureStatusNone) {
+        set_error("po2q: autotune synchronises the stream; run it before graph capture");
+        return PO2Q_ERR_INVALID;
+    }
+    hipEvent_t e0, e1;
+    st = hip_status(hipEventCreate(&e0), "event create");
+    if (st) return st;
+    if ((st = hip_status(hipEventCreate(&e1), "event create"))) {
+        (void)hipEventDestroy(e0);
+        return st;
+    }
+    // Two passes over the candidates, each run timed on its own and the minimum kept:
+    // the first candidates of a cold GPU run at ramping clocks, so a single pass
+    // would favour late candidates.
+    constexpr int kPasses = 2, kReps = 2;
+    int best = -1;
+    std::vector<float> tmin(cands.size(), 1e30f);
+    for (int pass = 0; pass < kPasses && !st; ++pass) {
+        for (int i = 0; i < (int)cands.size() && !st; ++i) {
+            st = run_plan(cands[i], x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes, s);  // untimed
+            for (int r = 0; r < kReps && !st; ++r) {
+                st = hip_status(hipEventRecord(e0, s), "event record");
+                if (!st) st = run_plan(cands[i], x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes, s);
+                if (!st) st = hip_status(hipEventRecord(e1, s), "event record");
+                if (!st) st = hip_status(hipEventSynchronize(e1), "autotune run");
+                float ms = 0.f;
+                if (!st) st = hip_status(hipEventElapsedTime(&ms, e0, e1), "event time");
+                if (!st) tmin[i] = std::min(tmin[i], ms);
+            }
+        }
+    }
+    for (int i = 0; i < (int)cands.size(); ++i)
+        if (best < 0 || tmin[i] < tmin[best]) best = i;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (st) return st;
+    tuned_store(cands[best], mode, bits, fsr, flags);
+    if (buf && len) describe_plan(cands[best], buf, len);
+    // leave y holding the chosen plan's output
+    return run_plan(cands[best], x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes, s);
+}
+
+int po2q_qconv2d_plans(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                       int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h,
+                       int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags, int index, char* buf,
+                       size_t len) {
+    std::vector<ConvPlan> cands;
+    if (!plan_candidates(cands, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags))
+        return -(flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID);
+    if (buf && len && index >= 0 && index < (int)cands.size()) describe_plan(cands[index], buf, len);
+    return (int)cands.size();
+}
+
+int po2q_qconv2d_f32_plan(int index, const float* x, const float* w, const float* bias, float* y, int64_t N,
+                          int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h,
+                          int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w,
+                          int64_t groups, int bits, int fsr, int mode, int flags, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+    int st = check_conv_args(x, w, y, workspace, mode, bits, flags);
+    if (st) return st;
+    std::vector<ConvPlan> cands;
+    if (!plan_candidates(cands, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    if (index < 0 || index >= (int)cands.size()) {
+        set_error("po2q: plan index " + std::to_string(index) + " out of range [0, " +
+                  std::to_string(cands.size()) + ")");
+        return PO2Q_ERR_INVALID;
+    }
+    return run_plan(cands[index], x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
 int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
                           int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w, int64_t dil_h,
                           int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags, char* buf,
@@ -166,12 +289,7 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
     if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
                    flags))
         return PO2Q_ERR_INVALID;
-    static const char* kinds[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma"};
-    snprintf(buf, len,
-             "kind=%s CC=%d NT=%d MI=%d NJ=%d vr=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
-             "lds=%zu blocks=%lld waves=%d",
-             kinds[p.kind], p.CC, p.NT, p.MI, p.NJ, p.vrx, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW, p.nchunks, p.kblocks,
-             p.steps, p.lds_bytes, (long long)p.blocks, p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4);
+    describe_plan(p, buf, len);
     return PO2Q_OK;
 }
 

@@ -13,7 +13,10 @@
 
 #include <algorithm>
 #include <climits>
+#include <array>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "po2q_internal.h"
 
@@ -179,9 +182,10 @@ __global__ __launch_bounds__(kThreads) void conv_depthwise(const float* __restri
 // ------------------------------------------------------------------ planning --
 static int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
-bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
-               int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t groups, int mode,
-               int bits, int fsr, int flags) {
+// Geometry validation (the reference's F.conv2d error conditions) and derived sizes.
+static bool plan_geometry(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                          int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                          int64_t groups) {
     if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || K <= 0 || R <= 0 || S <= 0 || groups <= 0) {
         set_error("po2q: all sizes must be positive");
         return false;
@@ -212,14 +216,65 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
 
     p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S; p.vrx = 0;
     p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0;
-    // bf16x3 split-exact MFMA (po2q_conv_x3.hip): default for quantized weights
-    if (flags == 2 || (flags == 0 && mode != 0 && !(p.Cg == 1 && groups > 1))) {
-        if (plan_bf16x3(p, mode, bits, fsr)) {
+    return true;
+}
+
+static bool bf16x3_wanted(const ConvPlan& p, int mode, int flags) {
+    return flags == 2 || (flags == 0 && mode != 0 && !(p.Cg == 1 && p.groups > 1));
+}
+
+// Any PO2Q_* tile/kernel tuning knob set: the planners obey it and the autotune cache is bypassed.
+static bool tuning_knobs() {
+    return getenv("PO2Q_X3_TILE") || getenv("PO2Q_X3P_TILE") || getenv("PO2Q_X3P_WAVES") || getenv("PO2Q_NO_DMA");
+}
+
+// Heuristic kernel choice between the two bf16x3 kernels, from the per-layer sweeps
+// (profiles/r01_v3_tile_sweep.jsonl): the LDS-DMA kernel wins on stride-2 3x3 layers
+// and on 3x3 stride-1 layers with 17..32 output channels, the register-staged kernel
+// elsewhere.  po2q_qconv2d_autotune replaces this with a measurement.
+static bool prefer_dma(const ConvPlan& p) {
+    if (getenv("PO2Q_X3P_TILE") || getenv("PO2Q_X3P_WAVES")) return true;
+    if (getenv("PO2Q_X3_TILE")) return false;
+    if (p.R == 3 && p.S == 3 && p.sh == 2 && p.sw == 2) return true;
+    return p.R == 3 && p.S == 3 && p.sh == 1 && p.sw == 1 && p.K > 16 && p.K <= 32;
+}
+
+// ------------------------------------------------------------ autotune cache --
+using PlanKey = std::array<int64_t, 18>;
+static std::mutex g_tuned_mu;
+static std::map<PlanKey, ConvPlan> g_tuned;
+
+static PlanKey plan_key(const ConvPlan& p, int mode, int bits, int fsr, int flags) {
+    return {p.N, p.C, p.H, p.W, p.K, p.R, p.S, p.sh, p.sw, p.ph, p.pw, p.dh, p.dw, p.groups, mode, bits, fsr, flags};
+}
+
+void tuned_store(const ConvPlan& p, int mode, int bits, int fsr, int flags) {
+    std::lock_guard<std::mutex> g(g_tuned_mu);
+    g_tuned[plan_key(p, mode, bits, fsr, flags)] = p;
+}
+
+static bool tuned_lookup(ConvPlan& p, int mode, int bits, int fsr, int flags) {
+    std::lock_guard<std::mutex> g(g_tuned_mu);
+    auto it = g_tuned.find(plan_key(p, mode, bits, fsr, flags));
+    if (it == g_tuned.end()) return false;
+    p = it->second;
+    return true;
+}
+
+static bool plan_fallback(ConvPlan& p);
+
+// Heuristic plan + the ranked bf16x3 alternatives (empty unless bf16x3 applies).
+static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, std::vector<PlanCand>* reg_out,
+                           std::vector<PlanCand>* dma_out) {
+    if (bf16x3_wanted(p, mode, flags)) {
+        std::vector<PlanCand> reg, dma;
+        x3_candidates(p, mode, bits, fsr, reg);
+        if (!reg.empty()) {
             const char* nd = getenv("PO2Q_NO_DMA");  // A/B knob: keep the register-staged kernel
-            if (!(nd && nd[0] == '1')) {
-                ConvPlan q = p;
-                if (plan_bf16x3_dma(q)) p = q;
-            }
+            if (!(nd && nd[0] == '1')) x3p_candidates(p, dma);
+            p = (!dma.empty() && prefer_dma(p)) ? dma[0].plan : reg[0].plan;
+            if (reg_out) *reg_out = std::move(reg);
+            if (dma_out) *dma_out = std::move(dma);
             return true;
         }
         if (flags == 2) {
@@ -228,6 +283,45 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
             return false;
         }
     }
+    return plan_fallback(p);
+}
+
+bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+               int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t groups, int mode,
+               int bits, int fsr, int flags) {
+    if (!plan_geometry(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups)) return false;
+    if (!tuning_knobs() && tuned_lookup(p, mode, bits, fsr, flags)) return true;
+    return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
+}
+
+constexpr int kTuneRegCands = 6, kTuneDmaCands = 8;
+
+bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                     int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                     int64_t groups, int mode, int bits, int fsr, int flags) {
+    ConvPlan p;
+    if (!plan_geometry(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups)) return false;
+    std::vector<PlanCand> reg, dma;
+    if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma)) return false;
+    out.clear();
+    out.push_back(p);
+    auto add = [&](const std::vector<PlanCand>& v, int n) {
+        for (int i = 0; i < (int)v.size() && i < n; ++i) {
+            const ConvPlan& c = v[i].plan;
+            bool dup = false;
+            for (const ConvPlan& o : out)
+                dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
+                       o.dma_waves == c.dma_waves;
+            if (!dup) out.push_back(c);
+        }
+    };
+    add(reg, kTuneRegCands);
+    add(dma, kTuneDmaCands);
+    return true;
+}
+
+static bool plan_fallback(ConvPlan& p) {
+    const int N = p.N, K = p.K, R = p.R, S = p.S, P = p.P, Q = p.Q, groups = p.groups;
     if (p.Cg == 1 && groups > 1) {  // depthwise
         p.kind = KIND_DEPTHWISE;
         p.MI = p.NJ = 1;

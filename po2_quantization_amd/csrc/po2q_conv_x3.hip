@@ -36,7 +36,9 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "po2q_internal.h"
 #include "po2q_x3_dev.h"
@@ -359,31 +361,37 @@ static size_t x3_lds(const ConvPlan& p, int NT, int HH, int WW) {
     return (size_t)3 * plane + (size_t)p.steps * NT * 1024 + 64 * sizeof(int);
 }
 
-bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
-    if (mode == 0 || p.groups != 1) return false;
-    if (bits < 1 || bits > 16) return false;
+void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
+    if (mode == 0 || base.groups != 1) return;
+    if (bits < 1 || bits > 16) return;
     const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
-    if (lo < -126 || hi > 127) return false;  // +-2^e must be a normal bf16
+    if (lo < -126 || hi > 127) return;  // +-2^e must be a normal bf16
+    ConvPlan p = base;
     p.taps = p.R * p.S;
-    if (p.taps > 64) return false;
-    if ((int64_t)p.H * p.W * 4 * 32 >= (1LL << 31)) return false;  // 32-bit buffer offsets per chunk
+    if (p.taps > 64) return;
+    if ((int64_t)p.H * p.W * 4 * 32 >= (1LL << 31)) return;  // 32-bit buffer offsets per chunk
     p.CC = (p.taps == 1 && p.C > 16) ? 32 : 16;
     const int OCT = p.CC / 8;
     p.steps = cdiv(p.taps * OCT, 4);
     p.SB = 2 * p.CC;
     p.NT = p.K <= 16 ? 1 : (p.K <= 32 ? 2 : 4);
     while (p.NT > 1 && p.steps * p.NT * 64 > kWI * kThreads) p.NT >>= 1;
-    if (p.steps * p.NT * 64 > kWI * kThreads) return false;
+    if (p.steps * p.NT * 64 > kWI * kThreads) return;
     p.kblocks = cdiv(p.K, 16 * p.NT);
     p.nchunks = cdiv(p.C, p.CC);
+    p.kind = KIND_BF16X3;
+    p.vrx = 0; p.PS = 0; p.MI = 0;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = 0;
 
-    // tile search (override: PO2Q_X3_TILE="NJ,TP,TQ", a tuning knob; it must pass
+    // tile candidates (override: PO2Q_X3_TILE="NJ,TP,TQ", a tuning knob; it must pass
     // the same validity checks as every searched candidate)
-    int bestNJ = 0, bestTP = 0, bestTQ = 0;
-    double best = 1e300;
-    auto consider = [&](int nj, int tp, int tq, bool forced) {
+    const char* env = getenv("PO2Q_X3_TILE");
+    int fnj = 0, ftp = 0, ftq = 0;
+    bool forced = env && sscanf(env, "%d,%d,%d", &fnj, &ftp, &ftq) == 3;
+    auto consider = [&](int nj, int tp, int tq) {
         if (nj == 7 && p.NT > 1) return;  // > 256 VGPRs: spills
         if (tp < 1 || tq < 1 || tp * tq != 64 * nj) return;
+        if (forced && (nj != fnj || tp != ftp || tq != ftq)) return;
         const int px = 64 * nj;
         const int HH = (tp - 1) * p.sh + (p.R - 1) * p.dh + 1;
         const int WW = (tq - 1) * p.sw + (p.S - 1) * p.dw + 1;
@@ -404,34 +412,31 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
         cost += 0.02 * (8.0 / nj);  // per-tile fixed costs (barriers, descriptors)
         const double blocks = (double)p.N * p.kblocks * tP * tQ;
         if (blocks < 1024) cost += 0.5 * (1024 - blocks) / 1024;
-        if (forced) cost = -1.0;
-        if (cost < best) {
-            best = cost; bestNJ = nj; bestTP = tp; bestTQ = tq;
-        }
+        if (blocks > INT_MAX) return;
+        ConvPlan c = p;
+        c.NJ = nj; c.TP = tp; c.TQ = tq;
+        c.tilesP = tP; c.tilesQ = tQ;
+        c.HH = HH; c.WW = WW; c.WWp = WW;
+        c.plane = HH * WW * p.SB + 32;  // + zero slot + trash slot
+        c.lds_bytes = lds;
+        // packed bf16 fragments: [kb][chunk][ks][nt][lane][8] -> 4-byte words
+        c.packed_floats = (int64_t)p.kblocks * p.nchunks * p.steps * p.NT * 64 * 4;
+        c.blocks = (int64_t)blocks;
+        out.push_back({cost, c});
     };
-    const char* env = getenv("PO2Q_X3_TILE");
-    int fnj = 0, ftp = 0, ftq = 0;
-    if (env && sscanf(env, "%d,%d,%d", &fnj, &ftp, &ftq) == 3) consider(fnj, ftp, ftq, true);
-    if (best >= 0) {
-        const int njs[] = {1, 2, 4, 7};
+    const int njs[] = {1, 2, 4, 7};
+    for (int pass = 0; pass < 2 && out.empty(); ++pass, forced = false)  // an invalid override is ignored
         for (int nj : njs)
             for (int tq = 1; tq <= std::min(p.Q, 64 * nj); ++tq)
-                if ((64 * nj) % tq == 0) consider(nj, 64 * nj / tq, tq, false);
-    }
-    if (!bestNJ) return false;
-    p.kind = KIND_BF16X3;
-    p.NJ = bestNJ; p.TP = bestTP; p.TQ = bestTQ; p.vrx = 0;
-    p.tilesP = cdiv(p.P, p.TP);
-    p.tilesQ = cdiv(p.Q, p.TQ);
-    p.HH = (p.TP - 1) * p.sh + (p.R - 1) * p.dh + 1;
-    p.WW = (p.TQ - 1) * p.sw + (p.S - 1) * p.dw + 1;
-    p.plane = p.HH * p.WW * p.SB + 32;  // + zero slot + trash slot
-    p.lds_bytes = x3_lds(p, p.NT, p.HH, p.WW);
-    p.WWp = p.WW; p.PS = 0; p.MI = 0;
-    // packed bf16 fragments: [kb][chunk][ks][nt][lane][8] -> 4-byte words
-    p.packed_floats = (int64_t)p.kblocks * p.nchunks * p.steps * p.NT * 64 * 4;
-    p.blocks = (int64_t)p.N * p.kblocks * p.tilesP * p.tilesQ;
-    if (p.blocks > INT_MAX) return false;
+                if ((64 * nj) % tq == 0) consider(nj, 64 * nj / tq, tq);
+    std::stable_sort(out.begin(), out.end(), [](const PlanCand& a, const PlanCand& b) { return a.cost < b.cost; });
+}
+
+bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
+    std::vector<PlanCand> c;
+    x3_candidates(p, mode, bits, fsr, c);
+    if (c.empty()) return false;
+    p = c[0].plan;
     return true;
 }
 

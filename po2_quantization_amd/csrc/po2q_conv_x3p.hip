@@ -502,11 +502,11 @@ static int cdivp(int a, int b) { return (a + b - 1) / b; }
 
 // Eligible: po2/po2+ (bf16x3 already planned), groups == 1, taps <= 64, W % 4 == 0,
 // a 16-byte-aligned input window per tile (TQ * stride % 4 == 0), K block bias in LDS.
-bool plan_bf16x3_dma(ConvPlan& p) {
+void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
     const char* wenv = getenv("PO2Q_X3P_WAVES");  // tuning knob: 4 or 8 waves per block
-    int best_waves = 0;
-    if (p.groups != 1 || p.taps > 64 || p.W % 4 || p.K > 1024) return false;
-    if ((int64_t)p.H * p.W * 4 * 16 >= (1LL << 31)) return false;
+    const ConvPlan& p = base;
+    if (p.groups != 1 || p.taps > 64 || p.W % 4 || p.K > 1024) return;
+    if ((int64_t)p.H * p.W * 4 * 16 >= (1LL << 31)) return;
     const bool vr_ok = p.R == 3 && p.S == 3 && p.sh == 1 && p.sw == 1 && p.dh == 1 && p.dw == 1 && p.K <= 16;
     const int cc = 16;
     const int nchunks = cdivp(p.C, cc);
@@ -515,9 +515,8 @@ bool plan_bf16x3_dma(ConvPlan& p) {
     while (NT > 1 && ksteps_k * NT * 64 > kPMaxNW * 4 * 64) NT >>= 1;
     const int kblocks = cdivp(p.K, 16 * NT);
     const bool mc = nchunks > 1 || kblocks > 1;
+    const int d0 = ((p.pw % 4) + 4) % 4 == 0 ? 0 : 4 - (p.pw % 4);  // w0 - aligned window start
 
-    double best = 1e300;
-    int bNJ = 0, bTP = 0, bTQ = 0, bVR = 0;
     const char* env = getenv("PO2Q_X3P_TILE");  // "NJ,TP,TQ,VRX" tuning knob
     int fnj = 0, ftp = 0, ftq = 0, fvr = -1;
     if (env && sscanf(env, "%d,%d,%d,%d", &fnj, &ftp, &ftq, &fvr) != 4) fvr = -1;
@@ -526,10 +525,11 @@ bool plan_bf16x3_dma(ConvPlan& p) {
         if (tp * tq != 16 * waves * nj) return;
         if ((tq * p.sw) % 4) return;
         if (vrx && (vrx > waves || tq != 16 * vrx || tp != nj * (waves / vrx))) return;
+        if (wenv && atoi(wenv) != waves) return;
+        if (fvr >= 0 && !(nj == fnj && tp == ftp && tq == ftq && vrx == fvr)) return;
         const int HH = (tp - 1) * p.sh + (p.R - 1) * p.dh + 1;
         const int WW = (tq - 1) * p.sw + (p.S - 1) * p.dw + 1;
         if (HH >= 4096 || WW >= 4096) return;
-        const int d0 = ((p.pw % 4) + 4) % 4 == 0 ? 0 : 4 - (p.pw % 4);  // w0 - aligned window start
         const int nck = cdivp(d0 + WW, 4);
         const int ni = cdivp(cc * HH * nck, 64 * waves);
         if (ni > kPMaxNI) return;
@@ -544,7 +544,6 @@ bool plan_bf16x3_dma(ConvPlan& p) {
         const size_t lds = (size_t)3 * plane + 2 * (size_t)raw_slot + (mc ? 3 : 1) * (size_t)w_slot + 4096 + 256;
         if (lds > 160 * 1024) return;
         const int bpc = (int)((160 * 1024) / lds);  // co-resident blocks per CU (LDS)
-        if (wenv && atoi(wenv) != waves) return;
         const int tP = cdivp(p.P, tp), tQ = cdivp(p.Q, tq);
         const double waste = (double)tP * tQ * tp * tq / ((double)p.P * p.Q);
         const double halo = (double)tP * tQ * HH * WW / ((double)p.P * p.Q * p.sh * p.sw);
@@ -552,10 +551,21 @@ bool plan_bf16x3_dma(ConvPlan& p) {
         if (bpc < 2) cost += 0.3;  // one block per CU: its barriers stall every wave in the same phase
         const double blocks = (double)p.N * kblocks * tP * tQ;
         if (blocks < 512) cost += 0.5 * (512 - blocks) / 512;
-        if (fvr >= 0) cost = (nj == fnj && tp == ftp && tq == ftq && vrx == fvr) ? -1.0 : 1e200;
-        if (cost < best) {
-            best = cost; bNJ = nj; bTP = tp; bTQ = tq; bVR = vrx; best_waves = waves;
-        }
+        if (blocks >= (1 << 20) || (double)tP * tQ >= (1 << 20)) return;  // udiv_magic range
+        ConvPlan c = p;
+        c.kind = KIND_BF16X3_DMA;
+        c.CC = cc; c.SB = 32; c.NT = NT; c.kblocks = kblocks; c.nchunks = nchunks;
+        c.NJ = nj; c.TP = tp; c.TQ = tq; c.vrx = vrx;
+        c.steps = steps;
+        c.tilesP = tP; c.tilesQ = tQ;
+        c.HH = HH; c.WW = WW; c.WWp = WW; c.PS = 0; c.MI = 0;
+        c.plane = plane;
+        c.dma_d0 = d0; c.dma_nck = nck; c.dma_waves = waves; c.dma_ni = ni;
+        c.dma_nw = mc ? nw : 0;
+        c.lds_bytes = lds;
+        c.packed_floats = (int64_t)kblocks * nchunks * steps * NT * 64 * 4;
+        c.blocks = (int64_t)blocks;
+        out.push_back({cost, c});
     };
     for (int waves : {4, 8})
         for (int nj : {1, 2, 4}) {
@@ -565,29 +575,15 @@ bool plan_bf16x3_dma(ConvPlan& p) {
             for (int vrx : {1, 2, 4, 8})
                 if (vrx <= waves) consider(waves, nj, nj * (waves / vrx), 16 * vrx, vrx);
         }
-    if (!bNJ || best > 1e100) return false;
-    p.kind = KIND_BF16X3_DMA;
-    p.CC = cc; p.SB = 32; p.NT = NT; p.kblocks = kblocks; p.nchunks = nchunks;
-    p.NJ = bNJ; p.TP = bTP; p.TQ = bTQ; p.vrx = bVR;
-    p.steps = bVR ? 15 : ksteps_k;
-    p.tilesP = cdivp(p.P, p.TP); p.tilesQ = cdivp(p.Q, p.TQ);
-    p.HH = (p.TP - 1) * p.sh + (p.R - 1) * p.dh + 1;
-    p.WW = (p.TQ - 1) * p.sw + (p.S - 1) * p.dw + 1;
-    p.WWp = p.WW; p.PS = 0; p.MI = 0;
-    p.plane = p.HH * p.WW * 32 + 32;
-    const int d0 = ((p.pw % 4) + 4) % 4 == 0 ? 0 : 4 - (p.pw % 4);
-    p.dma_d0 = d0;
-    p.dma_nck = cdivp(d0 + p.WW, 4);
-    p.dma_waves = best_waves;
-    p.dma_ni = cdivp(cc * p.HH * p.dma_nck, 64 * best_waves);
-    const int wfr = p.steps * NT * 64;
-    p.dma_nw = mc ? cdivp(wfr, 64 * best_waves) : 0;
-    const int raw_slot = p.dma_ni * best_waves * 1024;
-    const int w_slot = mc ? p.dma_nw * best_waves * 1024 : wfr * 16;
-    p.lds_bytes = (size_t)3 * p.plane + 2 * (size_t)raw_slot + (mc ? 3 : 1) * (size_t)w_slot + 4096 + 256;
-    p.packed_floats = (int64_t)kblocks * nchunks * p.steps * NT * 64 * 4;
-    p.blocks = (int64_t)p.N * kblocks * p.tilesP * p.tilesQ;
-    return p.blocks < (1 << 20) && p.tilesP * p.tilesQ < (1 << 20);  // udiv_magic range
+    std::stable_sort(out.begin(), out.end(), [](const PlanCand& a, const PlanCand& b) { return a.cost < b.cost; });
+}
+
+bool plan_bf16x3_dma(ConvPlan& p) {
+    std::vector<PlanCand> c;
+    x3p_candidates(p, c);
+    if (c.empty()) return false;
+    p = c[0].plan;
+    return true;
 }
 
 template <int WV, int NT, int NJ, int VRX, int KS, bool MC>

@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 namespace po2q {
 
@@ -52,16 +53,33 @@ struct ConvPlan {
     int64_t blocks;
 };
 
+// Default plan for a conv: the autotuned plan when po2q_qconv2d_autotune has
+// measured this problem in this process, else the planners' heuristic choice.
 bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                int64_t groups, int mode, int bits, int fsr, int flags);
 
-// bf16x3 planner (po2q_conv_x3.hip): fills the bf16x3 fields of an already
-// validated plan; false if the shape / exponent range is not eligible.
+// Every plan worth timing for this problem (heuristic default first); false on invalid input.
+bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
+                     int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
+                     int64_t dw, int64_t groups, int mode, int bits, int fsr, int flags);
+
+// Autotune cache: the measured-best plan per problem key (process-wide, thread-safe).
+void tuned_store(const ConvPlan& p, int mode, int bits, int fsr, int flags);
+
+struct PlanCand {
+    double cost;  // planner heuristic, lower is better
+    ConvPlan plan;
+};
+
+// bf16x3 register-staged candidates (po2q_conv_x3.hip), cost-ranked; empty if the
+// shape / exponent range is not eligible.  `base` is a validated geometry.
+void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out);
 bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr);
 
-// LDS-DMA pipelined bf16x3 plan (po2q_conv_x3p.hip): refines a bf16x3 plan; false if
-// the shape is not eligible (the po2q_conv_x3.hip plan is then kept).
+// LDS-DMA pipelined bf16x3 candidates (po2q_conv_x3p.hip), cost-ranked; empty if not
+// eligible.  Call only for problems x3_candidates accepts (same arithmetic).
+void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out);
 bool plan_bf16x3_dma(ConvPlan& p);
 
 // Pack (and quantize unless mode == 0) the weight into the plan's layout.

@@ -116,3 +116,23 @@ def test_bf16x3_eligibility_on_host():
     grouped = (2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 2)
     assert L.po2q_qconv2d_workspace_bytes(*grouped, 4, 1, 1, 2) == 0
     assert b"bf16x3" in L.po2q_last_error()
+
+
+def test_plan_enumeration_on_host():
+    """Autotune candidates: plan 0 is the heuristic default, every ResNet56 qconv
+    shape offers both bf16x3 kernels, invalid arguments report -status."""
+    shape = dict(N=256, C=16, H=224, W=224, K=16, R=3, S=3, stride=1, padding=1)
+    ps = _lib.plans(**shape)
+    assert len(ps) >= 2
+    assert ps[0] == _lib.describe(**shape)
+    assert any("kind=bf16x3 " in p for p in ps) and any("kind=bf16x3_dma" in p for p in ps)
+    assert len(set(ps)) == len(ps)
+    # plain (unquantized) conv: a single fp32 plan
+    assert _lib.plans(2, 16, 10, 10, 16, 3, 3, 1, 1, mode="none") == [_lib.describe(2, 16, 10, 10, 16, 3, 3, 1, 1,
+                                                                                     mode="none")]
+    L = _lib.load()
+    bad = (2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 3)  # groups does not divide C
+    assert L.po2q_qconv2d_plans(*bad, 4, 1, 1, 0, 0, None, 0) == -1
+    assert L.po2q_qconv2d_f32_plan(99, 1, 1, None, 1, 2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 1, 4, 1, 1, 0,
+                                   1, 1 << 20, None) == 1
+    assert b"out of range" in L.po2q_last_error()

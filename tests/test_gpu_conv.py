@@ -128,6 +128,72 @@ def test_full_size_resnet56_layers_vs_torch_fp32(layer):
     assert normwise_err(y[idx].cpu().numpy(), o) <= CONV_TOL
 
 
+PLAN_SHAPES = [s for s in SHAPES if s[-1] == 1]
+
+
+@pytest.mark.parametrize("shape", PLAN_SHAPES, ids=[str(s) for s in PLAN_SHAPES])
+def test_every_candidate_plan_vs_oracle(shape):
+    """Autotuning may select any candidate plan, so each one must meet the parity bar."""
+    N, C, H, W, K, R, S, st, pad, dil, groups = shape
+    g = torch.Generator().manual_seed(hash(shape) & 0xFFFF)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C // groups, R, S, generator=g) * 0.2
+    b = torch.randn(K, generator=g) * 0.1
+    ref, _ = O.qconv2d(x.numpy(), w.numpy(), b.numpy(), st, pad, dil, groups, 4, "po2+")
+    plans = _lib.plans(N, C, H, W, K, R, S, st, pad, dil, groups, 4, "po2+")
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    for i, desc in enumerate(plans):
+        y = _lib.qconv2d(xd, wd, bd, st, pad, dil, groups, 4, "po2+", plan=i).cpu().numpy()
+        assert normwise_err(y, ref) <= CONV_TOL, (desc, normwise_err(y, ref))
+
+
+@pytest.mark.parametrize("layer", FULL_LAYERS, ids=[str(l) for l in FULL_LAYERS])
+def test_full_size_every_candidate_plan(layer):
+    """BASELINE-size layers through every candidate plan vs torch fp32 conv of Q(w)."""
+    C, H, K, R, st, pad = layer
+    torch.manual_seed(1)
+    x = torch.randn(256, C, H, H, device=DEV)
+    w = torch.randn(K, C, R, R, device=DEV) * 0.1
+    ref = torch.nn.functional.conv2d(x, _lib.quantize(w, 4, "po2"), None, st, pad)
+    amax = ref.abs().max()
+    for i, desc in enumerate(_lib.plans(256, C, H, H, K, R, R, st, pad)):
+        y = _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=i)
+        err = ((y - ref).abs().max() / amax).item()
+        assert err <= CONV_TOL, (desc, err)
+        del y
+
+
+def test_autotune_picks_a_candidate_and_keeps_parity(monkeypatch):
+    """benchmark mode (cudnn.benchmark counterpart): the first call times every
+    candidate, later calls and describe() use the winner; results stay in parity."""
+    monkeypatch.setattr(_lib, "benchmark", True)
+    shape = (2, 16, 40, 36, 32, 3, 3, 1, 1, 1, 1)
+    N, C, H, W, K, R, S, st, pad, dil, groups = shape
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, R, S, generator=g) * 0.2
+    ref, _ = O.qconv2d(x.numpy(), w.numpy(), None, st, pad, dil, groups, 4, "po2")
+    plans = _lib.plans(N, C, H, W, K, R, S, st, pad, dil, groups, 4, "po2")
+    y1 = _lib.qconv2d(x.to(DEV), w.to(DEV), None, st, pad, dil, groups, 4, "po2").cpu().numpy()
+    assert normwise_err(y1, ref) <= CONV_TOL
+    chosen = _lib.describe(N, C, H, W, K, R, S, st, pad, dil, groups, 4, "po2")
+    assert chosen in plans
+    y2 = _lib.qconv2d(x.to(DEV), w.to(DEV), None, st, pad, dil, groups, 4, "po2").cpu().numpy()
+    assert np.array_equal(y1, y2)
+    # graph capture never autotunes (the sweep synchronises): a fresh shape is planned heuristically
+    with pytest.raises(RuntimeError, match="graph capture"):
+        L = _lib.load()
+        xs, ws_ = x.to(DEV), w.to(DEV)
+        y = torch.empty(N, K, H, W, device=DEV)
+        ws = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            st_ = L.po2q_qconv2d_autotune(xs.data_ptr(), ws_.data_ptr(), None, y.data_ptr(), N, C, H, W, K, R, S,
+                                          1, 1, 1, 1, 1, 1, 1, 4, 1, 1, 0, ws.data_ptr(), ws.numel(),
+                                          torch.cuda.current_stream().cuda_stream, None, 0)
+        _lib._check(st_)
+
+
 def test_backward_matches_torch_ste():
     torch.manual_seed(1)
     x = torch.randn(4, 16, 12, 12, device=DEV, requires_grad=True)

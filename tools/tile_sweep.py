@@ -1,6 +1,6 @@
-"""Sweep bf16x3 conv tile shapes (PO2Q_X3_TILE="NJ,TP,TQ") for each distinct
-ResNet56 qconv shape at the bench configuration; prints the planner's choice
-and every candidate's median time (HIP events).  Tuning aid, GPU only."""
+"""Time every candidate plan (po2q_qconv2d_plans: both bf16x3 kernels, ranked tile
+shapes) for each distinct ResNet56 qconv shape at the bench configuration, and
+what the autotuner picks.  Tuning aid, GPU only; one JSON line per shape."""
 import argparse
 import json
 import os
@@ -30,6 +30,12 @@ def timeit(fn, iters):
     return sorted(x.elapsed_time(y) for x, y in ev)[iters // 2]
 
 
+def short(desc):
+    f = dict(kv.split("=") for kv in desc.split())
+    k = "dma%s" % f["waves"] if f["kind"] == "bf16x3_dma" else ("reg" if f["kind"] == "bf16x3" else f["kind"])
+    return "%s NJ=%s vr=%s %s" % (k, f["NJ"], f["vr"], f["tile"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -42,50 +48,23 @@ def main():
         x = torch.randn(args.batch, C, H, H, device=dev)
         w = torch.randn(K, C, R, R, device=dev) * 0.1
         P = (H + 2 * pad - R) // st + 1
-        os.environ.pop("PO2Q_X3_TILE", None)
-        plan = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
-        t_auto = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
+        plans = _lib.plans(args.batch, C, H, H, K, R, R, st, pad)
         res = []
-        # LDS-DMA kernel (po2q_conv_x3p.hip): 4 or 8 waves, tile = 16 * waves * NJ pixels
-        for waves in (4, 8):
-            os.environ["PO2Q_X3P_WAVES"] = str(waves)
-            for nj in (1, 2, 4):
-                px = 16 * waves * nj
-                cands = [(px // tq, tq, 0) for tq in (4, 8, 16, 32, 64, 128) if px % tq == 0]
-                cands += [(nj * (waves // vrx), 16 * vrx, vrx) for vrx in (1, 2, 4, 8) if vrx <= waves]
-                for tp, tq, vrx in cands:
-                    os.environ["PO2Q_X3P_TILE"] = "%d,%d,%d,%d" % (nj, tp, tq, vrx)
-                    d = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
-                    if "bf16x3_dma" not in d or "tile=%dx%d" % (tp, tq) not in d or ("vr=%d" % vrx) not in d:
-                        continue
-                    t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
-                    res.append((t, "dma%d%s" % (waves, "vr%d" % vrx if vrx else ""), nj, tp, tq))
-        os.environ.pop("PO2Q_X3P_TILE", None)
-        os.environ.pop("PO2Q_X3P_WAVES", None)
-        os.environ["PO2Q_NO_DMA"] = "1"
-        for nj in (1, 2, 4, 7):
-            px = 64 * nj
-            for tq in sorted({8, 16, 32, 56, 64, 112, P, 4}):
-                if tq > P or px % tq or px // tq > 2 * P:
-                    continue
-                os.environ["PO2Q_X3_TILE"] = "%d,%d,%d" % (nj, px // tq, tq)
-                try:
-                    d = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
-                    if "tile=%dx%d" % (px // tq, tq) not in d:
-                        continue
-                    t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
-                except RuntimeError as e:
-                    continue
-                res.append((t, "reg", nj, px // tq, tq))
-        os.environ.pop("PO2Q_X3_TILE", None)
-        os.environ.pop("PO2Q_NO_DMA", None)
-        res.sort(key=lambda r: r[0])
+        for i, d in enumerate(plans):
+            t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=i), args.iters)
+            res.append((t, i, short(d)))
+        _lib.benchmark = True
+        _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2")  # autotune
+        _lib.benchmark = False
+        tuned = _lib.describe(args.batch, C, H, H, K, R, R, st, pad)
+        t_tuned = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), args.iters)
         flops = 2.0 * args.batch * K * P * P * C * R * R
         nbytes = 4.0 * (args.batch * C * H * H + args.batch * K * P * P + K * C * R * R)
-        print(json.dumps({"shape": [C, H, K, R, st], "auto_plan": plan, "auto_ms": round(t_auto, 4),
-                          "auto_GBs": round(nbytes / t_auto / 1e6, 1),
-                          "auto_TFs": round(flops / t_auto / 1e9, 1),
-                          "best": [(round(r[0], 4),) + tuple(r[1:]) for r in res[:8]]}), flush=True)
+        print(json.dumps({"shape": [C, H, K, R, st], "default": short(plans[0]), "default_ms": round(res[0][0], 4),
+                          "tuned": short(tuned), "tuned_ms": round(t_tuned, 4),
+                          "tuned_GBs": round(nbytes / t_tuned / 1e6, 1),
+                          "tuned_TFs": round(flops / t_tuned / 1e9, 1),
+                          "plans": [(round(r[0], 4), r[1], r[2]) for r in sorted(res)]}), flush=True)
         del x, w
 
 
