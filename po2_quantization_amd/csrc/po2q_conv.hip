@@ -215,7 +215,7 @@ static bool plan_geometry(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t 
     p.groups = (int)groups; p.P = (int)P; p.Q = (int)Q; p.Cg = (int)(C / groups); p.Kg = (int)(K / groups);
 
     p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S; p.vrx = 0;
-    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0; p.dma_ov = 0;
     return true;
 }
 
@@ -294,7 +294,7 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
     return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
 }
 
-constexpr int kTuneRegCands = 6, kTuneDmaCands = 8;
+constexpr int kTuneRegCands = 6, kTuneDmaCands = 12;
 
 bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                      int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
@@ -311,7 +311,8 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             bool dup = false;
             for (const ConvPlan& o : out)
                 dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
-                       o.dma_waves == c.dma_waves;
+                       o.dma_waves == c.dma_waves && o.dma_ov == c.dma_ov &&
+                       o.dma_nw == c.dma_nw;
             if (!dup) out.push_back(c);
         }
     };

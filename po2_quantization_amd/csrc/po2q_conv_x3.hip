@@ -381,7 +381,7 @@ void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
     p.nchunks = cdiv(p.C, p.CC);
     p.kind = KIND_BF16X3;
     p.vrx = 0; p.PS = 0; p.MI = 0;
-    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = 0;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = p.dma_ov = 0;
 
     // tile candidates (override: PO2Q_X3_TILE="NJ,TP,TQ", a tuning knob; it must pass
     // the same validity checks as every searched candidate)

@@ -124,7 +124,7 @@ __device__ __forceinline__ TileCoord tile_of_p(int v, const X3PArgs& a) {
     return t;
 }
 
-template <int WV, int NT, int NJ, int VRX, int KS, bool MC>
+template <int WV, int NT, int NJ, int VRX, int KS, bool MC, bool OV>
 __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                          const float* __restrict__ scale_p,
                                                          const float* __restrict__ bias, float* __restrict__ y,
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
     const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
 
     // ---- one-time LDS init: zero slots, tap table, bias
-    if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.plane + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < (OV ? 6 : 3)) *reinterpret_cast<uint4*>(lds + tid * a.plane + zero_off) = make_uint4(0u, 0u, 0u, 0u);
     int* tapt = reinterpret_cast<int*>(lds + a.tap_off);
     if (!VR && !KS && tid < a.taps) {
         const int r = tid / a.S, s = tid - (tid / a.S) * a.S;
@@ -286,10 +286,10 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
     Item i0{v0, 0, true, tile_of_p(v0, a)};
     Item i1 = next_item(i0);
     int wslot = 0;  // weight slot of i0 (multi-chunk ring of 3)
-    if constexpr (!MC) {  // one (k-block, chunk) for the whole launch: weights -> LDS once
+    if constexpr (!MC) {  // one k-block for the whole launch: every chunk's weights -> LDS once
         uint4* wl0 = reinterpret_cast<uint4*>(lds + a.w_off);
         const uint4* src = wpk + ((int64_t)i0.tc.kb * a.nchunks) * kfr;
-        for (int e = tid; e < kfr; e += (WV * 64)) wl0[e] = src[e];
+        for (int e = tid; e < kfr * a.nchunks; e += (WV * 64)) wl0[e] = src[e];
     }
     __syncthreads();  // LDS init + weights visible; plain loads all retired (vmcnt(0))
     bf16x8 bvr[VR ? 15 : 1];
@@ -298,16 +298,50 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         for (int f = 0; f < 15; ++f)
             bvr[f] = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(lds + a.w_off)[f * 64 + lane]);
     }
-    issue_x(i0, 0);
-    if constexpr (MC) issue_w(i0, 0);
-    issue_x(i1, 1);
-    if constexpr (MC) issue_w(i1, 1);
+    // split of one thread's r-th item: raw fp32 (8 channels) -> bf16 hi / mid / lo planes
+    auto split_one = [&](int r, const unsigned char* raw, unsigned char* pl) __attribute__((always_inline)) {
+        if (r * (WV * 64) < items) {  // block-uniform
+            uint32_t b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = *reinterpret_cast<const uint32_t*>(raw + sraw[r] + j * raw_cstride);
+            uint4 hi, mid, lo;
+            split3(b, hi, mid, lo);
+            *reinterpret_cast<uint4*>(pl + spl[r]) = hi;
+            *reinterpret_cast<uint4*>(pl + a.plane + spl[r]) = mid;
+            *reinterpret_cast<uint4*>(pl + 2 * a.plane + spl[r]) = lo;
+        }
+    };
     const int per_item = a.ni + (MC ? a.nw : 0);
+    const int pset = 3 * a.plane;  // bytes per plane set (OV: two sets)
+    int rslot = 0;   // raw slot of i0
+    int younger;     // vm ops issued after the DMA the loop top waits for
+    int pcur = 0;    // OV: plane set holding i0
+    Item i2;         // OV: the item after i1 (its x DMA is in flight)
+    if constexpr (OV) {
+        // Overlapped pipeline: raw ring of 3, plane sets of 2.  Iteration j (item i0)
+        // waits for x(i1) and w(i0), then issues x(i0 + 3) and w(i0 + 2) and runs the
+        // MFMAs of i0 interleaved with the split of i1 -- one barrier per item.
+        issue_x(i0, 0);
+        if constexpr (MC) issue_w(i0, 0);
+        issue_x(i1, 1);
+        wait_vmcnt(a.ni + (MC ? a.nw : 0));  // x(i0) landed
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int r = 0; r < kPXS; ++r) split_one(r, lds + a.raw_off, lds);
+        i2 = next_item(i1);
+        if constexpr (MC) issue_w(i1, 1);
+        issue_x(i2, 2);
+        younger = a.ni + (MC ? a.nw : 0);
+    } else {
+        issue_x(i0, 0);
+        if constexpr (MC) issue_w(i0, 0);
+        issue_x(i1, 1);
+        if constexpr (MC) issue_w(i1, 1);
+        younger = per_item;  // next item's DMA (+ stores)
+    }
 
     TileCoord done_tc = i0.tc;
     bool done = false;
-    int rslot = 0;  // raw slot of i0
-    int younger = per_item;  // vm ops issued after this item's DMA: next item's DMA (+ stores)
     const int st_per_tile = NJ * NT * (a.vec ? 1 : 4);
 
     // Every lane stores on every (nt, g): lanes without an output write to a dummy
@@ -358,37 +392,35 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         // (1) this item's DMA has landed (the next item's DMA may stay in flight), and
         //     every wave is past the previous item's MFMAs
         PO2Q_STAMP(0);
+        if constexpr (OV) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's split writes
         wait_vmcnt(younger);
         PO2Q_STAMP(1);
         __builtin_amdgcn_s_barrier();
         PO2Q_STAMP(2);
-        // (2) split: raw fp32 -> bf16 hi / mid / lo planes
-        if (!(a.dbg & 2)) {
-            const unsigned char* raw = lds + a.raw_off + rslot * a.raw_slot;
+        // (2) split: raw fp32 -> bf16 hi / mid / lo planes (OV: interleaved with the MFMAs below)
+        if constexpr (!OV) {
+            if (!(a.dbg & 2)) {
+                const unsigned char* raw = lds + a.raw_off + rslot * a.raw_slot;
 #pragma unroll
-            for (int r = 0; r < kPXS; ++r) {
-                if (r * (WV * 64) < items) {  // block-uniform
-                    uint32_t b[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        b[j] = *reinterpret_cast<const uint32_t*>(raw + sraw[r] + j * raw_cstride);
-                    uint4 hi, mid, lo;
-                    split3(b, hi, mid, lo);
-                    *reinterpret_cast<uint4*>(lds + spl[r]) = hi;
-                    *reinterpret_cast<uint4*>(lds + a.plane + spl[r]) = mid;
-                    *reinterpret_cast<uint4*>(lds + 2 * a.plane + spl[r]) = lo;
-                }
+                for (int r = 0; r < kPXS; ++r) split_one(r, raw, lds);
             }
+            PO2Q_STAMP(3);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // planes complete, raw slot free
+            PO2Q_STAMP(4);
         }
-        PO2Q_STAMP(3);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // planes complete, raw slot free
-        PO2Q_STAMP(4);
-        const unsigned char* wcur = lds + a.w_off + (MC ? wslot * a.w_slot : 0);
-        if constexpr (VR && MC) {
+        const unsigned char* pl = lds + pcur * pset;  // planes of i0
+        const int rnext = (rslot == 2) ? 0 : rslot + 1;
+        const unsigned char* raw_n = lds + a.raw_off + rnext * a.raw_slot;  // OV: raw of i1
+        unsigned char* pl_n = lds + (pcur ^ 1) * pset;                      // OV: planes for i1
+        const bool do_split = OV && !(a.dbg & 2);
+        const unsigned char* wcur = lds + a.w_off + (MC ? wslot * a.w_slot : i0.chunk * kfr * 16);
+        if constexpr (VR) {
+            if (MC || a.nchunks > 1) {
 #pragma unroll
-            for (int f = 0; f < 15; ++f)
-                bvr[f] = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(wcur)[f * 64 + lane]);
+                for (int f = 0; f < 15; ++f)
+                    bvr[f] = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(wcur)[f * 64 + lane]);
+            }
         }
         // (3) stores of the previous tile (older than the next DMA in vmcnt order)
         const int nst = (done && !(a.dbg & 8)) ? st_per_tile : 0;
@@ -398,10 +430,20 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         }
         PO2Q_STAMP(5);
         younger = nst + per_item;  // after the next item's DMA: these stores + the DMA below
-        // (4) DMA of the item after next into the raw slot just split (+ its weights)
-        const Item i2 = next_item(i1);
+        // (4) DMA of the item after next into the raw slot just split (+ its weights);
+        //     OV: x of the item three ahead, weights of the item two ahead
+        Item i3;
+        if constexpr (OV) {
+            i3 = next_item(i2);
+        } else {
+            i2 = next_item(i1);
+        }
         if (!(a.dbg & 4)) {
-            issue_x(i2, rslot);
+            if constexpr (OV) {
+                issue_x(i3, rslot);
+            } else {
+                issue_x(i2, rslot);
+            }
             if constexpr (MC) issue_w(i2, wslot == 0 ? 2 : wslot - 1);  // (wslot + 2) % 3
         } else {
             younger = nst;
@@ -418,7 +460,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
             const int l2 = upper ? zero_off : (hp0[0] + 2) * 32 + oct16 + 2 * a.plane;
             const int l2s = upper ? 0 : rowb;
             auto ld = [&](int ad) __attribute__((always_inline)) {
-                return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + ad));
+                return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pl + ad));
             };
             bf16x8 cur[5], nxt[5];
             cur[0] = ld(hm); cur[1] = ld(hm + 32); cur[2] = ld(hm + 64); cur[3] = ld(l01); cur[4] = ld(l2);
@@ -438,6 +480,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
                             acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[f], bvr[r * 5 + f], acc[i][0], 0, 0, 0);
                     }
                 }
+                if (ir < kPXS && do_split) split_one(ir, raw_n, pl_n);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int f = 0; f < 5; ++f) cur[f] = nxt[f];
@@ -451,10 +494,10 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
 #pragma unroll
                 for (int g = 0; g < NJ; ++g) {
                     const int ad = pad ? zero_off : x_addr<CC>(hp0[g] + toff, coct);
-                    const bf16x8 a0 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + ad));
-                    const bf16x8 a1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + a.plane + ad));
+                    const bf16x8 a0 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pl + ad));
+                    const bf16x8 a1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pl + a.plane + ad));
                     const bf16x8 a2 =
-                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + 2 * a.plane + ad));
+                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pl + 2 * a.plane + ad));
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt) {
                         acc[g][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[nt], acc[g][nt], 0, 0, 0);
@@ -465,8 +508,17 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
             };
             if constexpr (KS > 0) {
 #pragma unroll
-                for (int ks = 0; ks < KS; ++ks) kstep(ks, tpx[ks], tco[ks], (padm >> ks) & 1u);
+                for (int ks = 0; ks < KS; ++ks) {
+                    kstep(ks, tpx[ks], tco[ks], (padm >> ks) & 1u);
+                    if (ks < kPXS && do_split) split_one(ks, raw_n, pl_n);
+                }
+                if (KS < kPXS && do_split)
+#pragma unroll
+                    for (int r = KS; r < kPXS; ++r) split_one(r, raw_n, pl_n);
             } else {
+                if (do_split)
+#pragma unroll
+                    for (int r = 0; r < kPXS; ++r) split_one(r, raw_n, pl_n);
                 for (int ks = 0; ks < ksteps; ++ks) {
                     const int oi = ks * 4 + o;
                     const int t = oi / OCT;
@@ -486,7 +538,13 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         if (!i1.valid) break;
         i0 = i1;
         i1 = i2;
-        rslot ^= 1;
+        if constexpr (OV) {
+            i2 = i3;
+            rslot = rnext;
+            pcur ^= 1;
+        } else {
+            rslot ^= 1;
+        }
         if constexpr (MC) wslot = (wslot == 2) ? 0 : wslot + 1;
     }
     if (!(a.dbg & 8)) epilogue(done_tc);
@@ -514,13 +572,16 @@ void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
     int NT = p.K <= 16 ? 1 : (p.K <= 32 ? 2 : 4);
     while (NT > 1 && ksteps_k * NT * 64 > kPMaxNW * 4 * 64) NT >>= 1;
     const int kblocks = cdivp(p.K, 16 * NT);
-    const bool mc = nchunks > 1 || kblocks > 1;
+    const bool multi = nchunks > 1 || kblocks > 1;
     const int d0 = ((p.pw % 4) + 4) % 4 == 0 ? 0 : 4 - (p.pw % 4);  // w0 - aligned window start
 
     const char* env = getenv("PO2Q_X3P_TILE");  // "NJ,TP,TQ,VRX" tuning knob
     int fnj = 0, ftp = 0, ftq = 0, fvr = -1;
     if (env && sscanf(env, "%d,%d,%d,%d", &fnj, &ftp, &ftq, &fvr) != 4) fvr = -1;
-    auto consider = [&](int waves, int nj, int tp, int tq, int vrx) {
+    // mc: weights streamed per (k-block, chunk) item through a ring of 3 LDS slots;
+    // otherwise (one k-block) every chunk's weights stay resident in LDS for the launch
+    auto consider = [&](int waves, int nj, int tp, int tq, int vrx, bool ov, bool mc) {
+        if (mc != multi && !(multi && kblocks == 1)) return;
         if (vrx && (!vr_ok || NT != 1)) return;
         if (tp * tq != 16 * waves * nj) return;
         if ((tq * p.sw) % 4) return;
@@ -540,14 +601,15 @@ void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
         const int wfr = steps * NT * 64;
         const int nw = cdivp(wfr, 64 * waves);
         if (mc && nw > kPMaxNW) return;
-        const int w_slot = (mc ? nw * waves * 1024 : wfr * 16);
-        const size_t lds = (size_t)3 * plane + 2 * (size_t)raw_slot + (mc ? 3 : 1) * (size_t)w_slot + 4096 + 256;
+        const int w_slot = (mc ? nw * waves * 1024 : wfr * 16 * nchunks);
+        const size_t lds = (size_t)(ov ? 6 : 3) * plane + (ov ? 3 : 2) * (size_t)raw_slot +
+                           (mc ? 3 : 1) * (size_t)w_slot + 4096 + 256;
         if (lds > 160 * 1024) return;
         const int bpc = (int)((160 * 1024) / lds);  // co-resident blocks per CU (LDS)
         const int tP = cdivp(p.P, tp), tQ = cdivp(p.Q, tq);
         const double waste = (double)tP * tQ * tp * tq / ((double)p.P * p.Q);
         const double halo = (double)tP * tQ * HH * WW / ((double)p.P * p.Q * p.sh * p.sw);
-        double cost = waste + 0.35 * (halo - 1.0) + (vrx ? -0.2 : 0.0);
+        double cost = waste + 0.35 * (halo - 1.0) + (vrx ? -0.2 : 0.0) + (ov ? -0.1 : 0.0) + (mc ? 0.2 : 0.0);
         if (bpc < 2) cost += 0.3;  // one block per CU: its barriers stall every wave in the same phase
         const double blocks = (double)p.N * kblocks * tP * tQ;
         if (blocks < 512) cost += 0.5 * (512 - blocks) / 512;
@@ -562,6 +624,7 @@ void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
         c.plane = plane;
         c.dma_d0 = d0; c.dma_nck = nck; c.dma_waves = waves; c.dma_ni = ni;
         c.dma_nw = mc ? nw : 0;
+        c.dma_ov = ov ? 1 : 0;
         c.lds_bytes = lds;
         c.packed_floats = (int64_t)kblocks * nchunks * steps * NT * 64 * 4;
         c.blocks = (int64_t)blocks;
@@ -570,10 +633,13 @@ void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
     for (int waves : {4, 8})
         for (int nj : {1, 2, 4}) {
             const int px = 16 * waves * nj;
-            for (int tq = 4; tq <= std::min(p.Q + 3, px); tq += 4)
-                if (px % tq == 0) consider(waves, nj, px / tq, tq, 0);
-            for (int vrx : {1, 2, 4, 8})
-                if (vrx <= waves) consider(waves, nj, nj * (waves / vrx), 16 * vrx, vrx);
+            for (bool ov : {false, true})
+                for (bool mc : {false, true}) {
+                    for (int tq = 4; tq <= std::min(p.Q + 3, px); tq += 4)
+                        if (px % tq == 0) consider(waves, nj, px / tq, tq, 0, ov, mc);
+                    for (int vrx : {1, 2, 4, 8})
+                        if (vrx <= waves) consider(waves, nj, nj * (waves / vrx), 16 * vrx, vrx, ov, mc);
+                }
         }
     std::stable_sort(out.begin(), out.end(), [](const PlanCand& a, const PlanCand& b) { return a.cost < b.cost; });
 }
@@ -586,10 +652,10 @@ bool plan_bf16x3_dma(ConvPlan& p) {
     return true;
 }
 
-template <int WV, int NT, int NJ, int VRX, int KS, bool MC>
-static hipError_t launch_p(const ConvPlan& p, const X3PArgs& a, const float* x, const uint16_t* packed,
-                           const float* scale, const float* bias, float* y, hipStream_t s) {
-    auto kern = conv_x3p<WV, NT, NJ, VRX, KS, MC>;
+template <int WV, int NT, int NJ, int VRX, int KS, bool MC, bool OV>
+static hipError_t launch_p1(const ConvPlan& p, const X3PArgs& a, const float* x, const uint16_t* packed,
+                            const float* scale, const float* bias, float* y, hipStream_t s) {
+    auto kern = conv_x3p<WV, NT, NJ, VRX, KS, MC, OV>;
     if (p.lds_bytes > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
@@ -634,10 +700,17 @@ static hipError_t launch_p(const ConvPlan& p, const X3PArgs& a, const float* x, 
     return hipGetLastError();
 }
 
+template <int WV, int NT, int NJ, int VRX, int KS, bool MC>
+static hipError_t launch_p(const ConvPlan& p, const X3PArgs& a, const float* x, const uint16_t* packed,
+                           const float* scale, const float* bias, float* y, hipStream_t s) {
+    return p.dma_ov ? launch_p1<WV, NT, NJ, VRX, KS, MC, true>(p, a, x, packed, scale, bias, y, s)
+                    : launch_p1<WV, NT, NJ, VRX, KS, MC, false>(p, a, x, packed, scale, bias, y, s);
+}
+
 template <int WV, int NT, int NJ>
 static hipError_t launch_p_k(const ConvPlan& p, const X3PArgs& a, const float* x, const uint16_t* packed,
                              const float* scale, const float* bias, float* y, hipStream_t s) {
-    const bool mc = p.nchunks > 1 || p.kblocks > 1;
+    const bool mc = p.dma_nw > 0;  // weights streamed per item (else resident)
     if (p.steps == 5)
         return mc ? launch_p<WV, NT, NJ, 0, 5, true>(p, a, x, packed, scale, bias, y, s)
                   : launch_p<WV, NT, NJ, 0, 5, false>(p, a, x, packed, scale, bias, y, s);
@@ -649,7 +722,7 @@ template <int WV>
 static hipError_t launch_p_w(const ConvPlan& p, const X3PArgs& a, const float* x, const uint16_t* packed,
                              const float* scale, const float* bias, float* y, hipStream_t s) {
     if (p.vrx) {
-        const bool mcv = p.nchunks > 1;
+        const bool mcv = p.dma_nw > 0;
 #define PO2Q_PVR(NJ_, VRX_)                                                                         \
     if constexpr (VRX_ <= WV)                                                                       \
         if (p.NJ == NJ_ && p.vrx == VRX_)                                                           \
@@ -684,12 +757,12 @@ hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint1
     a.nchunks = p.nchunks; a.HH = p.HH; a.WW = p.WW; a.ksteps = p.steps; a.taps = p.taps;
     a.plane = p.plane;
     a.nck = p.dma_nck; a.d0 = p.dma_d0; a.ni = p.dma_ni; a.nw = p.dma_nw;
-    const bool mc = p.nchunks > 1 || p.kblocks > 1;
+    const bool mc = p.dma_nw > 0;
     const int wfr = p.steps * p.NT * 64;
-    a.raw_off = 3 * p.plane;
+    a.raw_off = (p.dma_ov ? 6 : 3) * p.plane;
     a.raw_slot = p.dma_ni * p.dma_waves * 1024;
-    a.w_off = a.raw_off + 2 * a.raw_slot;
-    a.w_slot = mc ? p.dma_nw * p.dma_waves * 1024 : wfr * 16;
+    a.w_off = a.raw_off + (p.dma_ov ? 3 : 2) * a.raw_slot;
+    a.w_slot = mc ? p.dma_nw * p.dma_waves * 1024 : wfr * 16 * p.nchunks;
     a.bias_off = a.w_off + (mc ? 3 : 1) * a.w_slot;
     a.tap_off = a.bias_off + 4096;
     a.vec = (p.Q % 4 == 0 && p.TQ % 4 == 0) ? 1 : 0;
