@@ -4,9 +4,10 @@ One step = one pass of the hot path over one batch: the 56 QuantizedConv2d
 layers of ResNet56 in graph order (each a fused PO2 quantize + conv, i.e. the
 reference's QuantizedConv2d.forward, models/quantized_conv.py:32-38), fed by
 the previous layer's output, then the classifier head (global avg-pool + fc).
-For N > 1 every rank runs its own batch shard (data-parallel inference: the
-path has no exchange step, so no collective in the timed region; only the
-barrier + max-over-ranks timing).  Inputs and weights are synthetic (seeded)
+For N > 1 every rank runs its own batch shard and the logits are gathered with
+an RCCL all_gather over xGMI (north_star: "inference batches shard across the
+GPUs with an RCCL all-gather of outputs"; 1 MB per rank, latency-bound).
+Inputs and weights are synthetic (seeded)
 and resident in HBM before the timed region.  Each conv shape is autotuned
 on its first (untimed, warmup) call, as the reference's cudnn.benchmark does.
 
@@ -151,6 +152,39 @@ def cpu_baseline(layers, weights_cpu, image, mode, bits, seconds):
                       "+ torch CPU F.conv2d/oneDNN, %d threads), %.1f s" % (reps, nb, image, image, threads, dt)}
 
 
+def gather_logits(logits, gathered, world):
+    """Output gather of the batch-sharded inference: rank r's logits land in rows
+    [r*B, (r+1)*B) of `gathered` on every rank (RCCL all_gather over xGMI)."""
+    if world > 1:
+        dist.all_gather_into_tensor(gathered, logits.contiguous())
+        return gathered
+    return logits
+
+
+def timed_steps(step, steps, warmup, world, sync, dev):
+    """`warmup` untimed steps, then exactly `steps` timed ones bracketed by a barrier +
+    device sync on both sides; returns the MAX wall time over ranks (seconds)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    return dt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,29 +221,15 @@ def main():
     chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
     B, Hs = args.batch, args.image
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
+    gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
 
     def step(record=False):
-        return chain.forward(x, record)
+        return gather_logits(chain.forward(x, record), gathered, world)
 
     with torch.no_grad():
-        for _ in range(max(args.warmup, 1 if _lib.benchmark else 0)):  # autotuning needs one untimed pass
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step(record=True)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+        # autotuning needs one untimed pass
+        dt = timed_steps(step, args.steps, max(args.warmup, 1 if _lib.benchmark else 0), world,
+                         torch.cuda.synchronize, dev)
 
     # dominant op: fused quantize+conv of the timed shape, HIP events on its stream
     ev_ms = [a.elapsed_time(b) for a, b in chain.events]
@@ -252,8 +272,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
-        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head"
-                               % (args.model, len(chain.layers), args.quantizer, args.bits),
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s"
+                               % (args.model, len(chain.layers), args.quantizer, args.bits,
+                                  " + RCCL all_gather(logits)" if world > 1 else ""),
                    "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
                    "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world},

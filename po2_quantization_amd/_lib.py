@@ -36,6 +36,11 @@ EXPORTS = (
 # None follows torch.backends.cudnn.benchmark, True / False force it.
 benchmark = None
 _tuned = set()
+# Optional persistent tuning record (the counterpart of a find-db): with
+# PO2Q_TUNE_FILE set, autotuned choices are saved as {problem key: plan index}
+# and reused by later processes (same library build, same candidate list).
+_tune_file = os.environ.get("PO2Q_TUNE_FILE")
+_tune_db = None
 
 _lib = None
 
@@ -167,14 +172,56 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
         if plan is not None:
             _check(L.po2q_qconv2d_f32_plan(int(plan), xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
                                            ws.data_ptr(), ws.numel(), _stream(xc.device)))
+        elif _saved_plan(key) is not None:
+            _check(L.po2q_qconv2d_f32_plan(_saved_plan(key), xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
+                                           ws.data_ptr(), ws.numel(), _stream(xc.device)))
         elif key not in _tuned and _benchmark_enabled():
+            buf = ctypes.create_string_buffer(512)
             _check(L.po2q_qconv2d_autotune(xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
-                                           ws.data_ptr(), ws.numel(), _stream(xc.device), None, 0))
+                                           ws.data_ptr(), ws.numel(), _stream(xc.device), buf, 512))
             _tuned.add(key)
+            _save_plan(key, buf.value.decode())
         else:
             _check(L.po2q_qconv2d_f32(xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
                                       ws.data_ptr(), ws.numel(), _stream(xc.device)))
     return y
+
+
+def _tune_key(key):
+    return ",".join(str(int(v)) for v in key)
+
+
+def _load_tune_db():
+    global _tune_db
+    if _tune_db is None:
+        _tune_db = {}
+        if _tune_file and os.path.exists(_tune_file):
+            import json
+            with open(_tune_file) as f:
+                _tune_db = json.load(f)
+    return _tune_db
+
+
+def _saved_plan(key):
+    if not _tune_file:
+        return None
+    return _load_tune_db().get(_tune_key(key))
+
+
+def _save_plan(key, desc):
+    if not _tune_file:
+        return
+    import json
+    L = load()
+    n = L.po2q_qconv2d_plans(*key, -1, None, 0)
+    buf = ctypes.create_string_buffer(512)
+    for i in range(max(n, 0)):
+        L.po2q_qconv2d_plans(*key, i, buf, 512)
+        if buf.value.decode() == desc:
+            _load_tune_db()[_tune_key(key)] = i
+            with open(_tune_file, "w") as f:
+                json.dump(_tune_db, f, indent=1, sort_keys=True)
+            return
 
 
 def _benchmark_enabled():

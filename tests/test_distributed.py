@@ -1,0 +1,59 @@
+"""N > 1 path of bench.py on CPU: world_size-2 gloo process group (127.0.0.1).
+
+Batch-sharded inference: every rank runs its own shard, the logits are gathered
+with all_gather (RCCL over xGMI on the GPU box, gloo here), and the step time is
+the MAX over ranks, measured between barriers (bench.py gather_logits /
+timed_steps)."""
+import os
+import socket
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    B, classes = 4, 10
+    w = torch.randn(16, classes, generator=torch.Generator().manual_seed(0))  # replicated "weights"
+    x = torch.randn(B, 16, generator=torch.Generator().manual_seed(100 + rank))  # this rank's shard
+    gathered = torch.empty(world * B, classes)
+    calls = []
+
+    def step(record=False):
+        calls.append(record)
+        time.sleep(0.05 * (rank + 1))  # rank 1 is the slow one
+        return bench.gather_logits(x @ w, gathered, world)
+
+    dt = bench.timed_steps(step, 3, 2, world, lambda: None, torch.device("cpu"))
+    torch.save({"dt": dt, "gathered": gathered.clone(), "calls": calls, "x": x}, os.path.join(out_dir, "r%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+def test_sharded_gather_and_max_over_ranks_timing(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / ("r%d.pt" % r), weights_only=True) for r in range(world)]
+    w = torch.randn(16, 10, generator=torch.Generator().manual_seed(0))
+    expect = torch.cat([res[r]["x"] @ w for r in range(world)])
+    for r in range(world):
+        assert torch.equal(res[r]["gathered"], expect)        # every rank holds every shard's logits
+        assert res[r]["calls"] == [False, False, True, True, True]  # W untimed, then exactly K timed steps
+    assert not torch.equal(res[0]["x"], res[1]["x"])           # distinct shards
+    assert res[0]["dt"] == res[1]["dt"]                        # one reported time: the max over ranks
+    assert res[0]["dt"] >= 3 * 0.1                             # covers the slower rank's 3 timed steps
+
+
+if __name__ == "__main__":
+    pytest.main([__file__, "-q"])

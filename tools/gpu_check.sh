@@ -6,6 +6,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# autotuned plans of the bench run are recorded here and reused by the profiling steps
+export PO2Q_TUNE_FILE=$PWD/gpurun_out/tune.json
 STEPS=${*:-smoke tests bench}
 
 run() {  # name timeout cmd...
@@ -36,6 +38,8 @@ for s in $STEPS; do
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
         counters) run counters 120 rocprofv3 -L ;;
+        traffic) run traffic 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" t1 "conv_x3p|conv_bf16x3" hbm
+                 python3 tools/traffic.py gpurun_out/pmc_t1 --algorithmic 1644185600 >> gpurun_out/traffic.log 2>&1 ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcd1) run pmcd1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" d1 ;;
         pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;

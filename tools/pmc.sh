@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC counter passes (one rocprofv3 run per counter group, kernel-trace only,
 # never combined with sys/runtime traces) over tools/prof_layer.py.
-# Usage: tools/pmc.sh "<prof_layer args>" [tag]
+# Usage: tools/pmc.sh "<prof_layer args>" [tag] [kernel regex] [all|hbm]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -19,6 +19,7 @@ GROUPS_=(
   "WRITE_SIZE"
   "TCC_HIT_sum TCC_MISS_sum"
 )
+if [ "${4:-all}" = hbm ]; then GROUPS_=("FETCH_SIZE" "WRITE_SIZE"); fi
 i=0
 for g in "${GROUPS_[@]}"; do
   i=$((i+1))

@@ -1,7 +1,10 @@
 """Run ONE fused quantize+conv layer a few times (for rocprofv3 kernel traces /
 PMC counters).  Shape defaults to ResNet56 stage 1 @224, bs=256.
 
-    python tools/prof_layer.py --shape 16,224,16,3,1,1 --iters 5 [--tile NJ,TP,TQ]
+    python tools/prof_layer.py --shape 16,224,16,3,1,1 --iters 5 [--plan I | --tile NJ,TP,TQ]
+
+Without --plan / --tile the layer is autotuned first (as bench.py does), so the
+profiled kernel is the plan the bench runs.
 """
 import argparse
 import os
@@ -20,6 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tile", default=None)
     ap.add_argument("--precision", default="auto")
+    ap.add_argument("--plan", type=int, default=None, help="candidate plan index (po2q_qconv2d_plans)")
     args = ap.parse_args()
     if args.tile:
         os.environ["PO2Q_X3_TILE"] = args.tile
@@ -29,9 +33,19 @@ def main():
     dev = torch.device("cuda:0")
     x = torch.randn(args.batch, C, H, H, device=dev)
     w = torch.randn(K, C, R, R, device=dev) * 0.1
-    print(_lib.describe(args.batch, C, H, H, K, R, R, st, pad, precision=args.precision), flush=True)
+    key = (args.batch, C, H, H, K, R, R, st, st, pad, pad, 1, 1, 1, 4, 1, 1, _lib.PRECISIONS[args.precision])
+    if args.plan is None and not args.tile and _lib._saved_plan(key) is not None:
+        args.plan = _lib._saved_plan(key)  # the plan bench.py tuned (PO2Q_TUNE_FILE)
+    if args.plan is None and not args.tile:
+        _lib.benchmark = True
+        _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", 1, args.precision)  # autotune
+        _lib.benchmark = False
+    desc = _lib.describe(args.batch, C, H, H, K, R, R, st, pad, precision=args.precision)
+    if args.plan is not None:
+        desc = _lib.plans(args.batch, C, H, H, K, R, R, st, pad, precision=args.precision)[args.plan]
+    print("PLAN " + desc, flush=True)
     for _ in range(args.iters):
-        _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", 1, args.precision)
+        _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", 1, args.precision, plan=args.plan)
     torch.cuda.synchronize()
 
 
