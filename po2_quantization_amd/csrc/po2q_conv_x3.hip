@@ -139,9 +139,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
     }
 
     uint32_t xr[kXI][8];
-    uint4 wr[MC ? kWI : 1];
+    // weight staging registers (multi-chunk): five named uint4s, not an array -- an
+    // array here was left dynamically indexed and lived in scratch memory
+    static_assert(kWI == 5, "weight staging is written out for kWI == 5");
+    uint4 wr0, wr1, wr2, wr3, wr4;
+#define PO2Q_W_ALL(OP) OP(0, wr0) OP(1, wr1) OP(2, wr2) OP(3, wr3) OP(4, wr4)
 
-    auto load_x = [&](const TileCoord& tc, int chunk) {
+    auto load_x = [&](const TileCoord& tc, int chunk) __attribute__((always_inline)) {
         const int h0 = tc.p0 * a.sh - a.ph, w0 = tc.q0 * a.sw - a.pw;
         const float* base = x + ((int64_t)tc.n * a.C + chunk * CC) * HWi;
         const int64_t rem = (int64_t)(a.C - chunk * CC) * HWi * 4;
@@ -165,14 +169,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
             for (int j = 0; j < 8; ++j) xr[r][j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * cstride, 0);
         }
     };
-    auto load_w = [&](int kb, int chunk) {
+    auto load_w = [&](int kb, int chunk) __attribute__((always_inline)) {
         const uint4* wc = wpk + ((int64_t)kb * a.nchunks + chunk) * kfr;
         if constexpr (MC) {
-#pragma unroll
-            for (int r = 0; r < kWI; ++r) {
-                const int e = tid + r * kThreads;
-                wr[r] = wc[e < kfr ? e : kfr - 1];
-            }
+#define PO2Q_W_LOAD(r, reg)                  \
+    {                                        \
+        const int e = tid + (r) * kThreads;  \
+        reg = wc[e < kfr ? e : kfr - 1];     \
+    }
+            PO2Q_W_ALL(PO2Q_W_LOAD)
+#undef PO2Q_W_LOAD
         } else {  // one (k-block, chunk) for the whole launch: straight to LDS, once
             uint4* wl0 = reinterpret_cast<uint4*>(lds + a.w_off);
             for (int e = tid; e < kfr; e += kThreads) wl0[e] = wc[e];
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), (short)0, bias ? a.K * 4 : 0, 0x00020000);
     float bias_next[NT], bias_done[NT];
-    auto load_bias = [&](int kb) {
+    auto load_bias = [&](int kb) __attribute__((always_inline)) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
             bias_next[nt] = __uint_as_float(
@@ -203,7 +209,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
     };
 
     // Epilogue of a finished tile: D[row = pixel 4*(lane>>4)+i][col = channel lane&15]
-    auto epilogue = [&](const TileCoord& tcs) {
+    auto epilogue = [&](const TileCoord& tcs) __attribute__((always_inline)) {
         const int64_t PQ = (int64_t)a.P * a.Q;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -274,11 +280,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
             *reinterpret_cast<uint4*>(lds + 2 * a.plane + ad) = lo;
         }
         if constexpr (MC) {
-#pragma unroll
-            for (int r = 0; r < kWI; ++r) {
-                const int e = tid + r * kThreads;
-                wl[e < kfr ? e : kfr - 1] = wr[r];
-            }
+#define PO2Q_W_STORE(r, reg)                 \
+    {                                        \
+        const int e = tid + (r) * kThreads;  \
+        wl[e < kfr ? e : kfr - 1] = reg;     \
+    }
+            PO2Q_W_ALL(PO2Q_W_STORE)
+#undef PO2Q_W_STORE
         }
         __syncthreads();
         if (chunk == 0) {  // bias of this tile arrived with its first chunk's x
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         if constexpr (MC) load_w(ntc.kb, lchunk);
 
         // ---- MFMAs over this chunk: k = (tap, channel), 32 per step
-        auto kstep = [&](int ks, int toff, int coct, bool pad) {
+        auto kstep = [&](int ks, int toff, int coct, bool pad) __attribute__((always_inline)) {
             bf16x8 bw[NT];
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
@@ -351,6 +359,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         tc = ntc;
     }
     if (!(a.dbg & 8)) epilogue(done_tc);
+#undef PO2Q_W_ALL
 }
 
 // ------------------------------------------------------------------ planning --
