@@ -90,8 +90,9 @@ class QConvChain:
         return torch.nn.functional.linear(pooled, self.fc_w, self.fc_b)
 
     def _timed(self, i, x, record):
-        if record and self.layers[i][1:3] == self.layers[self.timed_layer][1:3] and \
-                self.layers[i][3:6] == self.layers[self.timed_layer][3:6]:
+        # HIP events around the timed layer itself (one per step: an event pair costs
+        # ~10 us of queue time, so timing all 18 same-shape layers would slow the step)
+        if record and i == self.timed_layer:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()

@@ -161,74 +161,89 @@ __device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, in
     return bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
 }
 
-__global__ __launch_bounds__(kThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
+// 1024 threads: the fused absmax (every block reads the whole weight tensor from L2)
+// finishes in one or two rounds of independent loads per thread.
+constexpr int kPackThreads = 1024;
+
+__global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
                                                                const unsigned* __restrict__ partial,
                                                                int nparts, int lo, int hi, int mode,
                                                                PackX3 pg, uint16_t* __restrict__ packed,
                                                                float* __restrict__ scale_out) {
-    __shared__ unsigned red4[4];
+    __shared__ unsigned red[kPackThreads / 64];
     unsigned m = 0u;
     if (nparts > 0) {
-        for (int i = threadIdx.x; i < nparts; i += kThreads) m = max(m, partial[i]);
+        for (int i = threadIdx.x; i < nparts; i += kPackThreads) m = max(m, partial[i]);
     } else {  // fused absmax: every block reduces the whole (small, L2-resident) weight tensor
         const bool aligned = ((reinterpret_cast<uintptr_t>(w) & 15u) == 0);
-        int64_t i0 = 0;
+        int i0 = 0;  // the planner keeps fused weights below 2^20 elements
         if (aligned) {
-            const int64_t n4 = n >> 2;
+            const int n4 = (int)(n >> 2);
             const float4* w4 = reinterpret_cast<const float4*>(w);
-            for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
-                const float4 v = w4[i];
-                const unsigned a = __float_as_uint(v.x) & 0x7fffffffu, b = __float_as_uint(v.y) & 0x7fffffffu;
-                const unsigned c = __float_as_uint(v.z) & 0x7fffffffu, d = __float_as_uint(v.w) & 0x7fffffffu;
-                m = max(m, max(max(a, b), max(c, d)));
+            constexpr int U = 8;  // independent loads in flight per thread
+            for (int i = threadIdx.x; i < n4; i += U * kPackThreads) {
+                float4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = i + u * kPackThreads;
+                    v[u] = (k < n4) ? w4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const unsigned a = __float_as_uint(v[u].x) & 0x7fffffffu, b = __float_as_uint(v[u].y) & 0x7fffffffu;
+                    const unsigned c = __float_as_uint(v[u].z) & 0x7fffffffu, d = __float_as_uint(v[u].w) & 0x7fffffffu;
+                    m = max(m, max(max(a, b), max(c, d)));
+                }
             }
             i0 = n4 << 2;
         }
-        for (int64_t i = i0 + threadIdx.x; i < n; i += kThreads) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+        for (int i = i0 + threadIdx.x; i < (int)n; i += kPackThreads) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
     }
-    m = block_max_u32(m, red4);
+    m = block_max_u32<kPackThreads / 64>(m, red);
     const float scale = __uint_as_float(m);
     const bool fin = (m > 0u) && (m < 0x7f800000u);
     if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = fin ? scale : 1.0f;
+    // one 16-byte B fragment slot (8 consecutive k = 8 consecutive input channels of
+    // one tap, one output channel) per thread and iteration; 32-bit index math
     const int OCT = pg.CC >> 3;
-    const int64_t stride = (int64_t)gridDim.x * kThreads;
-    for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < pg.total; j += stride) {
-        int64_t t = j;
-        const int e8 = (int)(t & 7); t >>= 3;
-        const int lane = (int)(t & 63); t >>= 6;
+    const int RS = pg.R * pg.S;
+    const int nfr = (int)(pg.total >> 3);
+    uint4* out = reinterpret_cast<uint4*>(packed);
+    for (int j = blockIdx.x * kPackThreads + threadIdx.x; j < nfr; j += gridDim.x * kPackThreads) {
+        const int lane = j & 63;
+        int t = j >> 6;
+        int k, c0, tapoff;
+        bool ok;
         if (pg.vr) {
-            // row-reuse layout [chunk][r][f][lane][8], 3x3 / 16 output channels (po2q_conv_x3.hip):
+            // row-reuse layout [chunk][r][f][lane][8], 3x3 / 16 output channels (po2q_conv_x3p.hip):
             //   f = s in 0..2: B[k][n] = w[n][c][r][s] for both k halves (hi|mid A fragment)
             //   f = 3: k < 16 -> s = 0, k >= 16 -> s = 1;  f = 4: k < 16 -> s = 2, k >= 16 -> 0
-            const int fr = (int)(t % 15);
-            const int chunk = (int)(t / 15);
-            const int r = fr / 5, ft = fr % 5, grp = lane >> 4;
+            const int fr = t % 15, chunk = t / 15;
+            const int r = fr / 5, ft = fr - (fr / 5) * 5, grp = lane >> 4;
             const int sft = ft < 3 ? ft : (ft == 3 ? (grp >= 2 ? 1 : 0) : (grp >= 2 ? -1 : 2));
-            const int k = lane & 15;
-            const int c = chunk * 16 + 8 * (grp & 1) + e8;
-            uint16_t v = 0;
-            if (k < pg.K && c < pg.C && sft >= 0) {
-                const float wv = w[(((int64_t)k * pg.C + c) * 3 + r) * 3 + sft];
-                v = pack_one(wv, scale, fin, mode, lo, hi);
-            }
-            packed[j] = v;
-            continue;
+            k = lane & 15;
+            c0 = chunk * 16 + 8 * (grp & 1);
+            tapoff = r * 3 + sft;
+            ok = k < pg.K && sft >= 0;
+        } else {
+            const int nt = t % pg.NT; t /= pg.NT;
+            const int ks = t % pg.ksteps; t /= pg.ksteps;
+            const int chunk = t % pg.nchunks;
+            const int kb = t / pg.nchunks;
+            k = kb * 16 * pg.NT + nt * 16 + (lane & 15);
+            const int oi = ks * 4 + (lane >> 4);
+            const int tap = oi / OCT;
+            c0 = chunk * pg.CC + (oi - tap * OCT) * 8;
+            tapoff = tap;  // (r, s) row-major = tap
+            ok = k < pg.K && tap < pg.taps;
         }
-        const int nt = (int)(t % pg.NT); t /= pg.NT;
-        const int ks = (int)(t % pg.ksteps); t /= pg.ksteps;
-        const int chunk = (int)(t % pg.nchunks);
-        const int kb = (int)(t / pg.nchunks);
-        const int k = kb * 16 * pg.NT + nt * 16 + (lane & 15);
-        const int oi = ks * 4 + (lane >> 4);
-        const int tap = oi / OCT;
-        const int c = chunk * pg.CC + (oi - tap * OCT) * 8 + e8;
-        uint16_t v = 0;
-        if (k < pg.K && c < pg.C && tap < pg.taps) {
-            const int r = tap / pg.S, s = tap - (tap / pg.S) * pg.S;
-            const float wv = w[(((int64_t)k * pg.C + c) * pg.R + r) * pg.S + s];
-            v = pack_one(wv, scale, fin, mode, lo, hi);
+        uint32_t h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = c0 + e;
+            h[e] = (ok && c < pg.C) ? pack_one(w[(k * pg.C + c) * RS + tapoff], scale, fin, mode, lo, hi) : 0u;
         }
-        packed[j] = v;
+        out[j] = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
     }
 }
 
@@ -240,11 +255,11 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
     pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
     pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps; pg.vr = p.vrx ? 1 : 0;
     pg.total = p.packed_floats * 2;
-    int64_t b = (pg.total + 2047) / 2048;
+    int64_t b = (pg.total / 8 + kPackThreads - 1) / kPackThreads;  // one 16-byte fragment slot per thread
     if (b < 1) b = 1;
-    if (b > 40) b = 40;
+    if (b > 32) b = 32;
     const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
-    hipLaunchKernelGGL(pack_bf16x3_kernel, dim3((unsigned)b), dim3(kThreads), 0, s, w, n, partial, nparts, lo, hi,
+    hipLaunchKernelGGL(pack_bf16x3_kernel, dim3((unsigned)b), dim3(kPackThreads), 0, s, w, n, partial, nparts, lo, hi,
                        mode - 1, pg, packed, scale_out);
     return hipGetLastError();
 }

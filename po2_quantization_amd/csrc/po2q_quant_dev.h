@@ -62,14 +62,16 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 }
 
 // Block-wide max over 256 threads; every thread gets the result.
-__device__ __forceinline__ unsigned block_max_u32(unsigned v, unsigned* red4) {
+// Block-wide max of NW waves (red: NW LDS words).
+template <int NW = 4>
+__device__ __forceinline__ unsigned block_max_u32(unsigned v, unsigned* red) {
     v = wave_max_u32(v);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) red4[wave] = v;
+    if (lane == 0) red[wave] = v;
     __syncthreads();
-    unsigned m = red4[0];
+    unsigned m = red[0];
 #pragma unroll
-    for (int i = 1; i < 4; ++i) m = red4[i] > m ? red4[i] : m;
+    for (int i = 1; i < NW; ++i) m = red[i] > m ? red[i] : m;
     __syncthreads();
     return m;
 }
