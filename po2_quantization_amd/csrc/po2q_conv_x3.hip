@@ -52,6 +52,7 @@ struct X3Args {
     int plane;     // bytes per split plane (halo pixels * SB + 16 zero bytes)
     int w_off;     // LDS byte offset of the weight fragments
     int tap_off;   // LDS byte offset of the tap offset table
+    int bias_off;  // LDS byte offset of the bias (kblocks * 16 * NT floats, 0 past K)
     int vec;       // float4 epilogue allowed (Q % 4 == 0 && TQ % 4 == 0)
     int remap;     // XCD-aware block remap (nblocks % 8 == 0)
     int nblocks;
@@ -71,7 +72,7 @@ constexpr int kWI = 5;  // max weight fragments (uint4) per thread per chunk
 //   pixels outside the image and channels >= C get an out-of-range offset, so
 //   the hardware bounds check returns the zero padding.
 //   KS > 0: compile-time k-steps per chunk (tap offsets live in registers).
-template <int CC, int NT, int NJ, int KS, bool MC>
+template <int CC, int NT, int NJ, int KS, bool MC, int PD>
 __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restrict__ x,
                                                            const uint4* __restrict__ wpk,
                                                            const float* __restrict__ scale_p,
@@ -100,6 +101,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         tapt[tid] = r * a.dh * a.WW + s * a.dw;
     }
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.plane + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+    float* bias_l = reinterpret_cast<float*>(lds + a.bias_off);
+    for (int k = tid; k < a.kblocks * 16 * NT; k += kThreads) bias_l[k] = (bias && k < a.K) ? bias[k] : 0.0f;
 
     // halo pixel of this lane's pixel in each group (tile-linear, row-major);
     // epilogue position of its 4-pixel run
@@ -138,14 +141,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         pk[r] = (it < items) ? (0x80000000u | ((uint32_t)hh << 20) | ((uint32_t)ww << 8) | (uint32_t)oc) : 0u;
     }
 
-    uint32_t xr[kXI][8];
+    uint32_t xa[kXI][8], xb[PD == 2 ? kXI : 1][PD == 2 ? 8 : 1];
     // weight staging registers (multi-chunk): five named uint4s, not an array -- an
     // array here was left dynamically indexed and lived in scratch memory
     static_assert(kWI == 5, "weight staging is written out for kWI == 5");
     uint4 wr0, wr1, wr2, wr3, wr4;
 #define PO2Q_W_ALL(OP) OP(0, wr0) OP(1, wr1) OP(2, wr2) OP(3, wr3) OP(4, wr4)
 
-    auto load_x = [&](const TileCoord& tc, int chunk) __attribute__((always_inline)) {
+    auto load_x = [&](uint32_t (&xr)[kXI][8], const TileCoord& tc, int chunk) __attribute__((always_inline)) {
         const int h0 = tc.p0 * a.sh - a.ph, w0 = tc.q0 * a.sw - a.pw;
         const float* base = x + ((int64_t)tc.n * a.C + chunk * CC) * HWi;
         const int64_t rem = (int64_t)(a.C - chunk * CC) * HWi * 4;
@@ -195,19 +198,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
     uint4* wl = reinterpret_cast<uint4*>(lds + a.w_off);
     const int trash = zero_off + 16;  // per-plane 16-byte slot for padding items
 
-    // bias through a buffer descriptor: k >= K and bias == nullptr read 0 without a
-    // branch; loaded with the tile's x prefetch so the epilogue issues no loads (a
-    // load there would make every following store wait for all earlier stores)
-    const __amdgpu_buffer_rsrc_t brs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), (short)0, bias ? a.K * 4 : 0, 0x00020000);
-    float bias_next[NT], bias_done[NT];
-    auto load_bias = [&](int kb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            bias_next[nt] = __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(brs, (uint32_t)(kb * 16 * NT + nt * 16 + (lane & 15)) * 4u, 0, 0));
-    };
-
     // Epilogue of a finished tile: D[row = pixel 4*(lane>>4)+i][col = channel lane&15]
     auto epilogue = [&](const TileCoord& tcs) __attribute__((always_inline)) {
         const int64_t PQ = (int64_t)a.P * a.Q;
@@ -215,7 +205,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         for (int nt = 0; nt < NT; ++nt) {
             const int k = tcs.kb * 16 * NT + nt * 16 + (lane & 15);
             const bool kv = k < a.K;
-            const float bk = bias_done[nt];
+            const float bk = bias_l[tcs.kb * 16 * NT + nt * 16 + (lane & 15)];
             float* yk = y + ((int64_t)tcs.n * a.K + k) * PQ;
 #pragma unroll
             for (int g = 0; g < NJ; ++g) {
@@ -245,23 +235,46 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         }
     };
 
-    TileCoord tc = tile_of(v, a);
-    TileCoord done_tc = tc;  // tile whose finished sums sit in acc (stored one step later)
-    bool done = false;
-    int chunk = 0;
-    load_bias(tc.kb);
-    load_x(tc, 0);
-    load_w(tc.kb, 0);
-    float bias_cur[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) bias_cur[nt] = bias_done[nt] = 0.0f;
+    // Work items (tile v, chunk); past the end the "next" item repeats the last one
+    // (its prefetch is a harmless re-load), so no control-flow join follows a load.
+    struct Item {
+        int v, chunk;
+        bool valid;
+        TileCoord tc;
+    };
+    auto next_item = [&](const Item& it) __attribute__((always_inline)) {
+        Item n = it;
+        n.chunk = it.chunk + 1;
+        if (n.chunk == a.nchunks) {
+            n.chunk = 0;
+            n.v = it.v + (int)gridDim.x;
+        }
+        n.valid = it.valid && n.v < T;
+        if (!n.valid) {
+            n.v = it.v;
+            n.chunk = it.chunk;
+        } else if (n.v != it.v) {
+            n.tc = tile_of(n.v, a);
+        }
+        return n;
+    };
 
-    // Per work item, in this order (vmcnt counts loads AND stores in issue order, so
-    // the stores of the previous tile go out BEFORE the next prefetch: waiting for the
-    // prefetch at the top of the loop then never waits for just-issued stores):
+    Item cur{v, 0, true, tile_of(v, a)};
+    Item n1 = next_item(cur);
+    TileCoord done_tc = cur.tc;  // tile whose finished sums sit in acc (stored one step later)
+    bool done = false;
+    load_x(xa, cur.tc, 0);
+    load_w(cur.tc.kb, 0);
+    if constexpr (PD == 2) load_x(xb, n1.tc, n1.chunk);
+
+    // One work item, in this order (vmcnt counts loads AND stores in issue order, so
+    // the stores of the previous tile go out BEFORE the next prefetch: waiting for a
+    // prefetch at the split then never waits for just-issued stores):
     //   barrier | x regs -> split -> LDS, weights -> LDS | barrier |
-    //   stores of the previous tile | prefetch next item | MFMAs of this item
-    while (true) {
+    //   stores of the previous tile | prefetch (PD items ahead) | MFMAs of this item
+    // PD == 2 alternates two x register sets (xa: even items, xb: odd), so two items'
+    // loads are in flight across each MFMA phase.
+    auto step = [&](uint32_t (&xr)[kXI][8], const Item& it, const Item& pf) __attribute__((always_inline)) {
         __syncthreads();  // the previous item's MFMAs are done with LDS
 #pragma unroll
         for (int r = 0; r < kXI; ++r) {  // unconditional: padding items go to the trash slot
@@ -289,30 +302,18 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
 #undef PO2Q_W_STORE
         }
         __syncthreads();
-        if (chunk == 0) {  // bias of this tile arrived with its first chunk's x
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) bias_cur[nt] = bias_next[nt];
-        }
 
         if (done && !(a.dbg & 8)) {
             epilogue(done_tc);
             done = false;
         }
 
-        // ---- prefetch the next work item, unconditionally (past the end: a harmless
-        // re-load of the current item), so no control-flow join follows the loads
-        int nv = v, nchunk = chunk + 1;
-        if (nchunk == a.nchunks) {
-            nchunk = 0;
-            nv = v + gridDim.x;
+        // ---- prefetch: x of item `pf` into the registers just split, weights of the next item
+        load_x(xr, pf.tc, pf.chunk);
+        if constexpr (MC) {
+            const Item nw = PD == 2 ? n1 : pf;
+            load_w(nw.tc.kb, nw.chunk);
         }
-        const bool more = nv < T;
-        TileCoord ntc = tc;
-        if (nv != v) ntc = tile_of(more ? nv : v, a);
-        const int lchunk = more ? nchunk : chunk;
-        load_bias(ntc.kb);
-        load_x(ntc, lchunk);
-        if constexpr (MC) load_w(ntc.kb, lchunk);
 
         // ---- MFMAs over this chunk: k = (tap, channel), 32 per step
         auto kstep = [&](int ks, int toff, int coct, bool pad) __attribute__((always_inline)) {
@@ -347,16 +348,32 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
                 kstep(ks, pad ? 0 : tapt[t], oi % OCT, pad);
             }
         }
-        if (chunk == a.nchunks - 1) {
+        if (it.chunk == a.nchunks - 1) {
             done = true;
-            done_tc = tc;
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) bias_done[nt] = bias_cur[nt];
+            done_tc = it.tc;
         }
-        if (!more) break;
-        v = nv;
-        chunk = nchunk;
-        tc = ntc;
+    };
+
+    if constexpr (PD == 1) {
+        while (true) {
+            step(xa, cur, n1);
+            if (!n1.valid) break;
+            cur = n1;
+            n1 = next_item(n1);
+        }
+    } else {
+        while (true) {
+            Item n2 = next_item(n1);
+            step(xa, cur, n2);
+            if (!n1.valid) break;
+            cur = n1;
+            n1 = n2;
+            n2 = next_item(n1);
+            step(xb, cur, n2);
+            if (!n1.valid) break;
+            cur = n1;
+            n1 = n2;
+        }
     }
     if (!(a.dbg & 8)) epilogue(done_tc);
 #undef PO2Q_W_ALL
@@ -367,7 +384,8 @@ static int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 static size_t x3_lds(const ConvPlan& p, int NT, int HH, int WW) {
     const int plane = HH * WW * p.SB + 32;
-    return (size_t)3 * plane + (size_t)p.steps * NT * 1024 + 64 * sizeof(int);
+    return (size_t)3 * plane + (size_t)p.steps * NT * 1024 + 64 * sizeof(int) +
+           (size_t)p.kblocks * 16 * NT * sizeof(float);
 }
 
 void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
@@ -397,8 +415,9 @@ void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
     const char* env = getenv("PO2Q_X3_TILE");
     int fnj = 0, ftp = 0, ftq = 0;
     bool forced = env && sscanf(env, "%d,%d,%d", &fnj, &ftp, &ftq) == 3;
-    auto consider = [&](int nj, int tp, int tq) {
+    auto consider = [&](int nj, int tp, int tq, int pd) {
         if (nj == 7 && p.NT > 1) return;  // > 256 VGPRs: spills
+        if (pd == 2 && nj > 4) return;    // two x register sets: NJ <= 4
         if (tp < 1 || tq < 1 || tp * tq != 64 * nj) return;
         if (forced && (nj != fnj || tp != ftp || tq != ftq)) return;
         const int px = 64 * nj;
@@ -419,11 +438,13 @@ void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
         if (tq % 16 && tq != p.Q) cost += 0.05;
         if (tq % 4) cost += 0.1;
         cost += 0.02 * (8.0 / nj);  // per-tile fixed costs (barriers, descriptors)
+        if (pd == 2) cost -= 0.01;  // deeper prefetch: same tile, more loads in flight
         const double blocks = (double)p.N * p.kblocks * tP * tQ;
         if (blocks < 1024) cost += 0.5 * (1024 - blocks) / 1024;
         if (blocks > INT_MAX) return;
         ConvPlan c = p;
         c.NJ = nj; c.TP = tp; c.TQ = tq;
+        c.pd = pd;
         c.tilesP = tP; c.tilesQ = tQ;
         c.HH = HH; c.WW = WW; c.WWp = WW;
         c.plane = HH * WW * p.SB + 32;  // + zero slot + trash slot
@@ -437,7 +458,8 @@ void x3_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
     for (int pass = 0; pass < 2 && out.empty(); ++pass, forced = false)  // an invalid override is ignored
         for (int nj : njs)
             for (int tq = 1; tq <= std::min(p.Q, 64 * nj); ++tq)
-                if ((64 * nj) % tq == 0) consider(nj, 64 * nj / tq, tq);
+                if ((64 * nj) % tq == 0)
+                    for (int pd : {1, 2}) consider(nj, 64 * nj / tq, tq, pd);
     std::stable_sort(out.begin(), out.end(), [](const PlanCand& a, const PlanCand& b) { return a.cost < b.cost; });
 }
 
@@ -449,21 +471,30 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr) {
     return true;
 }
 
-template <int CC, int NT, int NJ, int KS, bool MC>
-static hipError_t launch_x3(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
-                            const float* scale, const float* bias, float* y, hipStream_t s) {
+template <int CC, int NT, int NJ, int KS, bool MC, int PD>
+static hipError_t launch_x3p(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
+                             const float* scale, const float* bias, float* y, hipStream_t s) {
     // persistent grid: as many blocks as can be co-resident (LDS / VGPR occupancy)
     int per_cu = 0, dev = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_bf16x3<CC, NT, NJ, KS, MC>, kThreads, p.lds_bytes) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_bf16x3<CC, NT, NJ, KS, MC, PD>, kThreads,
+                                                     p.lds_bytes) !=
             hipSuccess || per_cu < 1)
         per_cu = 1;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
         cus = 256;
     const int64_t grid = std::min<int64_t>(p.blocks, (int64_t)per_cu * cus);
-    hipLaunchKernelGGL((conv_bf16x3<CC, NT, NJ, KS, MC>), dim3((unsigned)grid), dim3(kThreads), p.lds_bytes, s, x,
-                       reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    hipLaunchKernelGGL((conv_bf16x3<CC, NT, NJ, KS, MC, PD>), dim3((unsigned)grid), dim3(kThreads), p.lds_bytes, s,
+                       x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
+}
+
+template <int CC, int NT, int NJ, int KS, bool MC>
+static hipError_t launch_x3(const ConvPlan& p, const X3Args& a, const float* x, const uint16_t* packed,
+                            const float* scale, const float* bias, float* y, hipStream_t s) {
+    if constexpr (NJ <= 4)
+        if (p.pd == 2) return launch_x3p<CC, NT, NJ, KS, MC, 2>(p, a, x, packed, scale, bias, y, s);
+    return launch_x3p<CC, NT, NJ, KS, MC, 1>(p, a, x, packed, scale, bias, y, s);
 }
 
 template <int CC, int NT, int NJ>
@@ -514,6 +545,7 @@ hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t*
     a.plane = p.plane;
     a.w_off = 3 * p.plane;
     a.tap_off = a.w_off + p.steps * p.NT * 1024;
+    a.bias_off = a.tap_off + 64 * (int)sizeof(int);
     a.vec = (p.Q % 4 == 0 && p.TQ % 4 == 0) ? 1 : 0;
     a.nblocks = (int)p.blocks;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;

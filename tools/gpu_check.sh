@@ -41,6 +41,8 @@ for s in $STEPS; do
         traffic) run traffic 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" t1 "conv_x3p|conv_bf16x3" hbm
                  python3 tools/traffic.py gpurun_out/pmc_t1 --algorithmic 1644185600 >> gpurun_out/traffic.log 2>&1 ;;
         stamps) run stamps 600 python tools/stamps.py ;;
+        pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
+        pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;
         pmcd1) run pmcd1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" d1 ;;
         pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;
         ablate) run ablate 600 bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
