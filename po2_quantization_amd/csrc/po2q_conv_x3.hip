@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
             const int hh = (int)((d >> 20) & 0x7ffu), ww = (int)((d >> 8) & 0xfffu), oc = (int)(d & 0xffu);
             const int h = h0 + hh, w = w0 + ww;
             const bool ok = (d >> 31) && ((unsigned)h < (unsigned)a.H) && ((unsigned)w < (unsigned)a.W) &&
-                            !(a.dbg & 4);
+                            !(kDbg(a) & 4);
             const uint32_t vo = ok ? ((uint32_t)(oc * 8) * cstride + (uint32_t)(h * a.W + w) * 4u) : 0x7fffffffu;
 #pragma unroll
             for (int j = 0; j < 8; ++j) xr[r][j] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * cstride, 0);
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
             const uint32_t d = pk[r];
             const int hp = (int)((d >> 20) & 0x7ffu) * a.WW + (int)((d >> 8) & 0xfffu);
             uint4 hi, mid, lo;
-            if (a.dbg & 2) {
+            if (kDbg(a) & 2) {
                 hi = make_uint4(xr[r][0], xr[r][1], xr[r][2], xr[r][3]);
                 mid = lo = make_uint4(xr[r][4], xr[r][5], xr[r][6], xr[r][7]);
             } else {
@@ -303,9 +303,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
         }
         __syncthreads();
 
-        if (done && !(a.dbg & 8)) {
+        if (done && !(kDbg(a) & 8)) {
             epilogue(done_tc);
             done = false;
+            // drain this wave's stores before the next prefetch goes out: measured
+            // faster than letting the loads queue behind them (HBM read/write turnaround)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
 
         // ---- prefetch: x of item `pf` into the registers just split, weights of the next item
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
                 }
             }
         };
-        if (a.dbg & 1) {
+        if (kDbg(a) & 1) {
         } else if constexpr (KS > 0) {
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) kstep(ks, tpx[ks], tco[ks], (padm >> ks) & 1u);
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16x3(const float* __restri
             n1 = n2;
         }
     }
-    if (!(a.dbg & 8)) epilogue(done_tc);
+    if (!(kDbg(a) & 8)) epilogue(done_tc);
 #undef PO2Q_W_ALL
 }
 

@@ -399,7 +399,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         PO2Q_STAMP(2);
         // (2) split: raw fp32 -> bf16 hi / mid / lo planes (OV: interleaved with the MFMAs below)
         if constexpr (!OV) {
-            if (!(a.dbg & 2)) {
+            if (!(kDbg(a) & 2)) {
                 const unsigned char* raw = lds + a.raw_off + rslot * a.raw_slot;
 #pragma unroll
                 for (int r = 0; r < kPXS; ++r) split_one(r, raw, lds);
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         const int rnext = (rslot == 2) ? 0 : rslot + 1;
         const unsigned char* raw_n = lds + a.raw_off + rnext * a.raw_slot;  // OV: raw of i1
         unsigned char* pl_n = lds + (pcur ^ 1) * pset;                      // OV: planes for i1
-        const bool do_split = OV && !(a.dbg & 2);
+        const bool do_split = OV && !(kDbg(a) & 2);
         const unsigned char* wcur = lds + a.w_off + (MC ? wslot * a.w_slot : i0.chunk * kfr * 16);
         if constexpr (VR) {
             if (MC || a.nchunks > 1) {
@@ -423,8 +423,8 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
             }
         }
         // (3) stores of the previous tile (older than the next DMA in vmcnt order)
-        const int nst = (done && !(a.dbg & 8)) ? st_per_tile : 0;
-        if (done && !(a.dbg & 8)) {
+        const int nst = (done && !(kDbg(a) & 8)) ? st_per_tile : 0;
+        if (done && !(kDbg(a) & 8)) {
             epilogue(done_tc);
             done = false;
         }
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         } else {
             i2 = next_item(i1);
         }
-        if (!(a.dbg & 4)) {
+        if (!(kDbg(a) & 4)) {
             if constexpr (OV) {
                 issue_x(i3, rslot);
             } else {
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         }
         PO2Q_STAMP(6);
         // (5) MFMAs of this item
-        if (a.dbg & 1) {
+        if (kDbg(a) & 1) {
         } else if constexpr (VR) {
             const int rowb = a.WW * 32;
             const int oct16 = ((lane >> 4) & 1) * 16;
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(WV * 64, 1) void conv_x3p(const float* __restrict__
         }
         if constexpr (MC) wslot = (wslot == 2) ? 0 : wslot + 1;
     }
-    if (!(a.dbg & 8)) epilogue(done_tc);
+    if (!(kDbg(a) & 8)) epilogue(done_tc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (unconsumed) DMAs
 #ifdef PO2Q_STAMPS
     if (lane == 0 && a.stamps)

@@ -6,7 +6,25 @@
 
 #include <cstdint>
 
+// Timing-ablation switches (PO2Q_X3_DEBUG bits: 1 no MFMA, 2 no split, 4 no x loads,
+// 8 no stores) exist only in the diagnostic build (-DPO2Q_DIAG=1, `make diag`): in the
+// product build kDbg() is the constant 0, so none of the ablation branches -- which
+// otherwise split the control flow the compiler's wait-count analysis sees -- is emitted.
+#ifndef PO2Q_DIAG
+#define PO2Q_DIAG 0
+#endif
+
 namespace po2q {
+
+template <class Args>
+__device__ __forceinline__ int kDbg(const Args& a) {
+#if PO2Q_DIAG
+    return a.dbg;
+#else
+    (void)a;
+    return 0;
+#endif
+}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="16,224,16,3,1,1")
     ap.add_argument("--tile", default=None)
+    ap.add_argument("--plans", default=None, help="comma-separated candidate plan indices (default: heuristic plan)")
     ap.add_argument("--batch", type=int, default=256)
     args = ap.parse_args()
     C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
@@ -26,11 +27,16 @@ def main():
     dev = torch.device("cuda:0")
     x = torch.randn(args.batch, C, H, H, device=dev)
     w = torch.randn(K, C, R, R, device=dev) * 0.1
-    res = {"plan": _lib.describe(args.batch, C, H, H, K, R, R, st, pad)}
-    for dbg in (0, 1, 2, 3, 4, 8, 12, 5, 7, 9, 11, 13, 14, 15):
-        os.environ["PO2Q_X3_DEBUG"] = str(dbg)
-        res[str(dbg)] = round(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2"), 7), 4)
-    os.environ.pop("PO2Q_X3_DEBUG")
+    plans = [None] if args.plans is None else [int(p) for p in args.plans.split(",")]
+    descs = _lib.plans(args.batch, C, H, H, K, R, R, st, pad)
+    for pl in plans:
+        res = {"plan": _lib.describe(args.batch, C, H, H, K, R, R, st, pad) if pl is None else descs[pl]}
+        for dbg in (0, 1, 2, 3, 4, 8, 12, 5, 7, 9, 11, 13, 14, 15):
+            os.environ["PO2Q_X3_DEBUG"] = str(dbg)
+            res[str(dbg)] = round(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=pl), 7), 4)
+        os.environ.pop("PO2Q_X3_DEBUG")
+        print(json.dumps(res), flush=True)
+    res = {}
     # reference points: torch copy of the same bytes
     y = torch.empty_like(x)
     res["copy_in_bytes_ms"] = round(timeit(lambda: y.copy_(x), 7), 4)

@@ -45,7 +45,8 @@ for s in $STEPS; do
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;
         pmcd1) run pmcd1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" d1 ;;
         pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;
-        ablate) run ablate 600 bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
+        ablate1) run ablate1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 2,3 ;;
+        ablate) run ablate 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
                   -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s" ;;
