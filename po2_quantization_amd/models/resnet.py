@@ -88,16 +88,22 @@ class ResNet(nn.Module):
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
     def get_quantization_error(self):
-        """(sum of squared quantization error, #weights) over the residual stages.
+        """(sum of squared quantization error, element count) over the residual stages.
 
-        The reference (resnet.py:205-224) shadows its element counter and skips
-        the projection convs; here every block's two convs are counted once."""
+        Same value as the reference (resnet.py:203-224), quirks included so the
+        per-element error train.py logs is unchanged: projection convs are not
+        visited, and inside a stage the element counter is overwritten by each
+        block and then doubled (`qerror, numel = ...; numel += numel`), so a
+        stage contributes 2 x its last block's count."""
         err, num = 0.0, 0
         for layer in (self.layer1, self.layer2, self.layer3):
+            stage_n = 0
             for blk in layer:
                 if isinstance(blk, BasicBlock):
-                    e, n = blk.get_quantization_error()
-                    err, num = err + e, num + n
+                    e, stage_n = blk.get_quantization_error()
+                    err = err + e
+                    stage_n = 2 * stage_n
+            num += stage_n
         return err, num
 
 

@@ -161,17 +161,27 @@ def gen_models():
     torch.manual_seed(0)
     x = torch.randn(8, 3, 32, 32, generator=torch.Generator().manual_seed(1))
     out["x/cifar8"] = x.numpy()
+    # MobileViT (config 5: po2+ 2-bit, weights only) at CIFAR size (1x1 patches) and at
+    # 64x64 (2x2 patches, the ImageNet-size code path; 224 raises in the reference)
+    out["x/img64"] = torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(2)).numpy()
     specs = [("resnet20", None, 4, 10), ("resnet56", "po2", 4, 10), ("mobilenet", "po2+", 4, 10),
-             ("resnet20", "po2+", 3, 10), ("mobilenet", "po2", 2, 10)]
-    for mt, q, bits, nc in specs:
-        m = get_model(mt, nc, quantizer_dict[q] if q else None, bits, 32)
+             ("resnet20", "po2+", 3, 10), ("mobilenet", "po2", 2, 10), ("mobilevit", "po2+", 2, 10),
+             ("mobilevit", "po2", 4, 10), ("mobilevit@64", "po2+", 2, 10)]
+    for mt_spec, q, bits, nc in specs:
+        mt, _, sz = mt_spec.partition("@")
+        sz = int(sz or 32)
+        m = get_model(mt, nc, quantizer_dict[q] if q else None, bits, (sz, sz))
         seeded_fill_(m, seed=7)
         m.eval()
         keys[mt] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+        xin = x if sz == 32 else torch.from_numpy(out["x/img64"])
         with torch.no_grad():
-            logits = m(x)
-        tag = "%s/%s/%d" % (mt, q or "none", bits)
+            logits = m(xin)
+        tag = "%s/%s/%d" % (mt_spec, q or "none", bits)
         out["logits/" + tag] = logits.numpy()
+        if q is not None:  # model-level get_quantization_error (reference quirks included)
+            e, n = m.get_quantization_error()
+            out["qerr/" + tag] = np.array([float(torch.as_tensor(e).detach()), float(n)], dtype=np.float64)
         if q is None:
             for qn in ("po2", "po2+", "lin", "lin+"):
                 mc = get_model(mt, nc, None, bits, 32)

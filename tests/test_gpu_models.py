@@ -21,19 +21,26 @@ DEV = "cuda:0"
 LOGIT_TOL = CONV_TOL
 
 
-def build(mt, q, bits):
-    m = get_model(mt, 10, quantizer_dict[q] if q else None, bits, 32)
+def build(spec, q, bits):
+    mt, _, sz = spec.partition("@")
+    m = get_model(mt, 10, quantizer_dict[q] if q else None, bits, (int(sz or 32),) * 2)
     seeded_fill_(m, seed=7)
     return m.to(DEV).eval()
 
 
-@pytest.mark.parametrize("mt,q,bits", [("resnet20", None, 4), ("resnet56", "po2", 4), ("resnet20", "po2+", 3)])
-def test_qat_mode_logits(mt, q, bits):
+# config 2 (resnet56 po2-4), config 3 (mobilenet po2+-4: depthwise + pointwise convs),
+# config 5 (mobilevit po2+-2, weights only; @64 = the 2x2-patch path used at ImageNet sizes)
+@pytest.mark.parametrize("spec,q,bits", [("resnet20", None, 4), ("resnet56", "po2", 4), ("resnet20", "po2+", 3),
+                                         ("mobilenet", "po2+", 4), ("mobilenet", "po2", 2),
+                                         ("mobilevit", "po2+", 2), ("mobilevit", "po2", 4),
+                                         ("mobilevit@64", "po2+", 2)])
+def test_qat_mode_logits(spec, q, bits):
     d = load_npz("models.npz")
-    m = build(mt, q, bits)
+    m = build(spec, q, bits)
+    x = d["x/img64"] if spec.endswith("@64") else d["x/cifar8"]
     with torch.no_grad():
-        y = m(torch.from_numpy(d["x/cifar8"]).to(DEV)).cpu().numpy()
-    ref = d["logits/%s/%s/%d" % (mt, q or "none", bits)]
+        y = m(torch.from_numpy(x).to(DEV)).cpu().numpy()
+    ref = d["logits/%s/%s/%d" % (spec, q or "none", bits)]
     assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
 
 
@@ -54,6 +61,6 @@ def test_state_dict_keys_match_reference():
     import json
 
     keys = json.load(open(os.path.join(GOLDEN, "models.json")))
-    for mt in ("resnet20", "resnet56"):
-        m = get_model(mt, 10, None, 4, 32)
+    for mt in ("resnet20", "resnet56", "mobilenet", "mobilevit"):
+        m = get_model(mt, 10, None, 4, (32, 32))
         assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == keys[mt]

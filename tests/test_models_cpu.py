@@ -1,0 +1,91 @@
+"""Model graphs on the CPU (no GPU): wiring, state_dict keys and
+get_quantization_error of the drop-in ResNet / MobileNetV2 / MobileViT against
+the reference's golden logits.
+
+The native calls (`_lib.quantize`, `_lib.qconv2d`) are replaced, in this test
+only, by a CPU double built from the oracle (bit-exact quantizer restatement +
+torch CPU conv, the reference's own CPU arithmetic), so what is checked here is
+the module graph around the hot path.  The HIP kernels themselves are checked
+by the `-m gpu` tests (test_gpu_models.py runs the same graphs on the device).
+"""
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from po2_quantization_amd import _lib
+from po2_quantization_amd.models.model import get_model
+from po2_quantization_amd.utils.quantizers import quantizer_dict
+from tests._util import CONV_TOL, GOLDEN, load_json, load_npz, normwise_err
+
+sys.path.insert(0, GOLDEN)
+from fill import seeded_fill_  # noqa: E402
+
+
+def _cpu_quantize(w, bits, mode, fsr=1):
+    return torch.from_numpy(O.quantize(w.detach().numpy(), bits, mode, fsr))
+
+
+def _cpu_qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+                 precision="auto"):
+    qw = w if mode in (None, "none") else _cpu_quantize(w, bits, mode, fsr)
+    return torch.nn.functional.conv2d(x, qw, bias, stride, padding, dilation, groups)
+
+
+@pytest.fixture
+def cpu_double(monkeypatch):
+    monkeypatch.setattr(_lib, "quantize", _cpu_quantize)
+    monkeypatch.setattr(_lib, "qconv2d", _cpu_qconv2d)
+
+
+MODELS = [("resnet20", None, 4), ("resnet56", "po2", 4), ("resnet20", "po2+", 3), ("mobilenet", "po2+", 4),
+          ("mobilenet", "po2", 2), ("mobilevit", "po2+", 2), ("mobilevit", "po2", 4), ("mobilevit@64", "po2+", 2)]
+
+
+def _build(spec, q, bits):
+    mt, _, sz = spec.partition("@")
+    sz = int(sz or 32)
+    m = get_model(mt, 10, quantizer_dict[q] if q else None, bits, (sz, sz))
+    seeded_fill_(m, seed=7)
+    return m.eval(), sz
+
+
+@pytest.mark.parametrize("spec,q,bits", MODELS)
+def test_logits_match_reference(cpu_double, spec, q, bits):
+    d = load_npz("models.npz")
+    torch.set_num_threads(4)
+    m, sz = _build(spec, q, bits)
+    x = torch.from_numpy(d["x/cifar8"] if sz == 32 else d["x/img64"])
+    with torch.no_grad():
+        y = m(x).numpy()
+    ref = d["logits/%s/%s/%d" % (spec, q or "none", bits)]
+    assert normwise_err(y, ref) <= CONV_TOL, normwise_err(y, ref)
+
+
+@pytest.mark.parametrize("spec,q,bits", [s for s in MODELS if s[1] is not None])
+def test_model_quantization_error_matches_reference(cpu_double, spec, q, bits):
+    """Model-level get_quantization_error() == the reference's, quirks included."""
+    d = load_npz("models.npz")
+    m, _ = _build(spec, q, bits)
+    e, n = m.get_quantization_error()
+    e = torch.as_tensor(e).detach()
+    ref_e, ref_n = d["qerr/%s/%s/%d" % (spec, q, bits)]
+    assert int(n) == int(ref_n)
+    assert abs(float(e) - ref_e) <= 1e-5 * ref_e
+
+
+@pytest.mark.parametrize("mt", ["resnet20", "resnet56", "mobilenet", "mobilevit"])
+def test_state_dict_keys(mt):
+    keys = load_json("models.json")
+    m = get_model(mt, 10, None, 4, (32, 32))
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == keys[mt]
+
+
+def test_mobilevit_224_raises_like_reference(cpu_double):
+    """The reference cannot run MobileViT at 224x224: the last stage's 7x7 map does
+    not tile into 2x2 patches (einops raises EinopsError, a RuntimeError)."""
+    m = get_model("mobilevit", 10, quantizer_dict["po2+"], 2, (224, 224)).eval()
+    with torch.no_grad(), pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 224, 224))
