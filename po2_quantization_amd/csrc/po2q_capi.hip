@@ -87,7 +87,8 @@ struct WsLayout {
 static WsLayout ws_layout(const ConvPlan& p, int mode) {
     WsLayout L;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA) && nw <= kFusedAbsmaxMax;
+    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) &&
+                       nw <= kFusedAbsmaxMax;
     L.nparts = (mode == PO2Q_MODE_NONE || fused) ? 0 : absmax_blocks(nw);
     L.part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
     L.scale_off = L.part_bytes;
@@ -147,15 +148,20 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         st = hip_status(launch_absmax(w, nw, partial, L.nparts, s), "absmax launch");
         if (st) return st;
     }
-    if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA) {
+    if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) {
         st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
                                            reinterpret_cast<uint16_t*>(packed), scale, s),
                         "weight pack launch");
         if (st) return st;
         const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
-        return hip_status(p.kind == KIND_BF16X3_DMA ? launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s)
-                                                    : launch_conv_bf16x3(p, x, pk, scale, bias, y, s),
-                          "conv launch");
+        hipError_t e;
+        if (p.kind == KIND_BF16X3_DMA)
+            e = launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s);
+        else if (p.kind == KIND_BF16X3_ROWS)
+            e = launch_conv_bf16x3_rows(p, x, pk, scale, bias, y, s);
+        else
+            e = launch_conv_bf16x3(p, x, pk, scale, bias, y, s);
+        return hip_status(e, "conv launch");
     }
     st = hip_status(launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
                     "weight pack launch");
@@ -163,7 +169,7 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     return hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
 }
 
-static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma"};
+static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows"};
 
 static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
     snprintf(buf, len,

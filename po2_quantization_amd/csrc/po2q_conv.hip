@@ -265,7 +265,7 @@ static bool plan_fallback(ConvPlan& p);
 
 // Heuristic plan + the ranked bf16x3 alternatives (empty unless bf16x3 applies).
 static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, std::vector<PlanCand>* reg_out,
-                           std::vector<PlanCand>* dma_out) {
+                           std::vector<PlanCand>* dma_out, std::vector<PlanCand>* rows_out = nullptr) {
     if (bf16x3_wanted(p, mode, flags)) {
         std::vector<PlanCand> reg, dma;
         x3_candidates(p, mode, bits, fsr, reg);
@@ -273,6 +273,7 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
             const char* nd = getenv("PO2Q_NO_DMA");  // A/B knob: keep the register-staged kernel
             if (!(nd && nd[0] == '1')) x3p_candidates(p, dma);
             p = (!dma.empty() && prefer_dma(p)) ? dma[0].plan : reg[0].plan;
+            if (rows_out) rows_candidates(p, mode, bits, fsr, *rows_out);
             if (reg_out) *reg_out = std::move(reg);
             if (dma_out) *dma_out = std::move(dma);
             return true;
@@ -294,15 +295,15 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
     return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
 }
 
-constexpr int kTuneRegCands = 6, kTuneDmaCands = 12;
+constexpr int kTuneRegCands = 6, kTuneDmaCands = 12, kTuneRowsCands = 3;
 
 bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                      int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                      int64_t groups, int mode, int bits, int fsr, int flags) {
     ConvPlan p;
     if (!plan_geometry(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups)) return false;
-    std::vector<PlanCand> reg, dma;
-    if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma)) return false;
+    std::vector<PlanCand> reg, dma, rows;
+    if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma, &rows)) return false;
     out.clear();
     out.push_back(p);
     auto add = [&](const std::vector<PlanCand>& v, int n) {
@@ -316,6 +317,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             if (!dup) out.push_back(c);
         }
     };
+    add(rows, kTuneRowsCands);
     add(reg, kTuneRegCands);
     add(dma, kTuneDmaCands);
     return true;

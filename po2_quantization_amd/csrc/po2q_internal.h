@@ -27,7 +27,7 @@ hipError_t launch_quantize_plain(const float* w, int64_t n, const unsigned* part
                                  int bits, int fsr, int mode, float* out, hipStream_t s);
 
 // Conv kinds
-enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2, KIND_BF16X3_DMA = 3 };
+enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2, KIND_BF16X3_DMA = 3, KIND_BF16X3_ROWS = 4 };
 
 // Conv geometry and tiling plan (host-side, shared by workspace sizing and launch).
 struct ConvPlan {
@@ -84,6 +84,10 @@ bool plan_bf16x3(ConvPlan& p, int mode, int bits, int fsr);
 void x3p_candidates(const ConvPlan& base, std::vector<PlanCand>& out);
 bool plan_bf16x3_dma(ConvPlan& p);
 
+// Row-streaming bf16x3 candidates (po2q_conv_rows.hip: 3x3 / stride 1 / C in {16, 32});
+// empty if not eligible.
+void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+
 // Pack (and quantize unless mode == 0) the weight into the plan's layout.
 hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned* partial, int nparts,
                                int bits, int fsr, int mode, float* packed, hipStream_t s);
@@ -99,6 +103,9 @@ hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, c
 
 hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t* packed,
                               const float* scale, const float* bias, float* y, hipStream_t s);
+
+hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed,
+                                   const float* scale, const float* bias, float* y, hipStream_t s);
 
 hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
                                   const float* scale, const float* bias, float* y, hipStream_t s);

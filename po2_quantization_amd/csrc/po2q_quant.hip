@@ -214,7 +214,26 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
         int t = j >> 6;
         int k, c0, tapoff;
         bool ok;
-        if (pg.vr) {
+        if (pg.vr == 2) {
+            // row-streaming layout [r][ks][nt][lane][8] (po2q_conv_rows.hip), one chunk:
+            //   CC = 16: ks 0 -> k < 16: s = 0, k >= 16: s = 1;  ks 1 -> k < 16: s = 2, else 0
+            //   CC = 32: ks = s, k = the 32 channels
+            const int nt = t % pg.NT;
+            const int ks = (t / pg.NT) % pg.ksteps;
+            const int r = t / (pg.NT * pg.ksteps);
+            const int grp = lane >> 4;
+            int sft;
+            if (pg.CC == 16) {
+                sft = ks == 0 ? (grp >> 1) : (grp < 2 ? 2 : -1);
+                c0 = 8 * (grp & 1);
+            } else {
+                sft = ks;
+                c0 = 8 * grp;
+            }
+            k = nt * 16 + (lane & 15);
+            tapoff = r * 3 + sft;
+            ok = k < pg.K && sft >= 0;
+        } else if (pg.vr) {
             // row-reuse layout [chunk][r][f][lane][8], 3x3 / 16 output channels (po2q_conv_x3p.hip):
             //   f = s in 0..2: B[k][n] = w[n][c][r][s] for both k halves (hi|mid A fragment)
             //   f = 3: k < 16 -> s = 0, k >= 16 -> s = 1;  f = 4: k < 16 -> s = 2, k >= 16 -> 0
@@ -253,7 +272,8 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
     clamp_window(bits, fsr, lo, hi);
     PackX3 pg;
     pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
-    pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps; pg.vr = p.vrx ? 1 : 0;
+    pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps;
+    pg.vr = p.kind == KIND_BF16X3_ROWS ? 2 : (p.vrx ? 1 : 0);
     pg.total = p.packed_floats * 2;
     int64_t b = (pg.total / 8 + kPackThreads - 1) / kPackThreads;  // one 16-byte fragment slot per thread
     if (b < 1) b = 1;

@@ -81,6 +81,12 @@ SHAPES = [
     (1, 8, 70, 70, 24, 3, 3, 1, 1, 1, 1),
     (3, 16, 8, 8, 16, 3, 3, 1, 1, 1, 1),
     (1, 12, 9, 9, 20, 5, 3, 2, (2, 1), 1, 4),
+    # row-streaming kernel edges: strip wider than the image, ragged last strip /
+    # segment, C = 32 -> K = 16, one-row images
+    (2, 16, 5, 4, 16, 3, 3, 1, 1, 1, 1),
+    (1, 16, 37, 68, 16, 3, 3, 1, 1, 1, 1),
+    (1, 32, 23, 20, 16, 3, 3, 1, 1, 1, 1),
+    (2, 32, 1, 12, 32, 3, 3, 1, 1, 1, 1),
 ]
 
 

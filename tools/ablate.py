@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--tile", default=None)
     ap.add_argument("--plans", default=None, help="comma-separated candidate plan indices (default: heuristic plan)")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--var", default="PO2Q_X3_DEBUG", help="ablation switch (PO2Q_ROWS_DEBUG for the row kernel)")
+    ap.add_argument("--values", default="0,1,2,3,4,8,12,5,7,9,11,13,14,15")
     args = ap.parse_args()
     C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
     if args.tile:
@@ -31,10 +33,10 @@ def main():
     descs = _lib.plans(args.batch, C, H, H, K, R, R, st, pad)
     for pl in plans:
         res = {"plan": _lib.describe(args.batch, C, H, H, K, R, R, st, pad) if pl is None else descs[pl]}
-        for dbg in (0, 1, 2, 3, 4, 8, 12, 5, 7, 9, 11, 13, 14, 15):
-            os.environ["PO2Q_X3_DEBUG"] = str(dbg)
+        for dbg in (int(v) for v in args.values.split(",")):
+            os.environ[args.var] = str(dbg)
             res[str(dbg)] = round(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=pl), 7), 4)
-        os.environ.pop("PO2Q_X3_DEBUG")
+        os.environ.pop(args.var)
         print(json.dumps(res), flush=True)
     res = {}
     # reference points: torch copy of the same bytes
