@@ -74,8 +74,12 @@ __device__ __forceinline__ void rows_dma4(__amdgpu_buffer_rsrc_t rs, uint32_t vo
                  : "memory");
 }
 // out-of-range voffset (>= the descriptor's size): the store is dropped, yet counted
+template <bool NTS = false>
 __device__ __forceinline__ void rows_store(__amdgpu_buffer_rsrc_t rs, uint32_t vo, floatx4 v) {
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
+    if constexpr (NTS)
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
+    else
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
 }
 template <int N>
 __device__ __forceinline__ void rows_wait() {
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                     const floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
                     const int q = q0 + 4 * b;
                     const uint32_t yo = (uint32_t)(nt * 16 + c) * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + q;
-                    rows_store(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
+                    rows_store<(DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
                 }
             }
             if (lane == 0) *reinterpret_cast<uint4*>(slab + zero_off) = make_uint4(0u, 0u, 0u, 0u);
@@ -331,7 +335,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                     v[1] = acc[D][grp][nt][1] * scale + bk[nt];
                     v[2] = acc[D][grp][nt][2] * scale + bk[nt];
                     v[3] = acc[D][grp][nt][3] * scale + bk[nt];
-                    rows_store(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    rows_store<(DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
             }
         }
@@ -348,11 +352,11 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
         load_row(0, 0);
         if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store(ry, 0x7fffffffu, z);
+            for (int i = 0; i < ST; ++i) rows_store<(DBG & 16) != 0>(ry, 0x7fffffffu, z);
         load_row(1, 1);
         if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store(ry, 0x7fffffffu, z);
+            for (int i = 0; i < ST; ++i) rows_store<(DBG & 16) != 0>(ry, 0x7fffffffu, z);
     }
     // steps past nrows DMA zeros (out of range) and store nothing: at most 5 per item
     for (int j = 0; j < nrows; j += 6) {
@@ -452,7 +456,7 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
     case d: return launch_rows_t<16, 1, d>(p, x, packed, scale, bias, y, s);
             PO2Q_ROWS_CASE(1) PO2Q_ROWS_CASE(2) PO2Q_ROWS_CASE(3) PO2Q_ROWS_CASE(4) PO2Q_ROWS_CASE(5)
             PO2Q_ROWS_CASE(6) PO2Q_ROWS_CASE(7) PO2Q_ROWS_CASE(8) PO2Q_ROWS_CASE(9) PO2Q_ROWS_CASE(12)
-            PO2Q_ROWS_CASE(13) PO2Q_ROWS_CASE(14) PO2Q_ROWS_CASE(15)
+            PO2Q_ROWS_CASE(13) PO2Q_ROWS_CASE(14) PO2Q_ROWS_CASE(15) PO2Q_ROWS_CASE(16) PO2Q_ROWS_CASE(20)
 #undef PO2Q_ROWS_CASE
             default: break;
         }

@@ -40,6 +40,13 @@ for s in $STEPS; do
         counters) run counters 120 rocprofv3 -L ;;
         traffic) run traffic 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" t1 "conv_x3p|conv_bf16x3" hbm
                  python3 tools/traffic.py gpurun_out/pmc_t1 --algorithmic 1644185600 >> gpurun_out/traffic.log 2>&1 ;;
+        traffic_rows)  # HBM bytes of the row-streaming stage-1 plans (candidate indices 1..3)
+                 cp profiles/traffic.json gpurun_out/traffic.json
+                 for i in 1 2 3; do
+                     run pmc_trows$i 300 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --plan $i" trows$i "conv_rows" hbm
+                     python3 tools/traffic.py gpurun_out/pmc_trows$i --algorithmic 1644185600 \
+                         --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
+                 done ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;

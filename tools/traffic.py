@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("pmc_dir")
     ap.add_argument("--algorithmic", type=float, default=None)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
     plan = None
     for name in sorted(os.listdir(args.pmc_dir)):
@@ -39,7 +40,7 @@ def main():
            "source": os.path.relpath(args.pmc_dir, ROOT)}
     if args.algorithmic:
         rec["traffic_over_algorithmic"] = round((rd + wr) / args.algorithmic, 3)
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    path = args.out
     db = json.load(open(path)) if os.path.exists(path) else {}
     db[plan] = rec
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
