@@ -272,8 +272,13 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
         if (!reg.empty()) {
             const char* nd = getenv("PO2Q_NO_DMA");  // A/B knob: keep the register-staged kernel
             if (!(nd && nd[0] == '1')) x3p_candidates(p, dma);
+            std::vector<PlanCand> rows;
+            rows_candidates(p, mode, bits, fsr, rows);
             p = (!dma.empty() && prefer_dma(p)) ? dma[0].plan : reg[0].plan;
-            if (rows_out) rows_candidates(p, mode, bits, fsr, *rows_out);
+            // the row-streaming kernels beat both tile kernels on every shape they take
+            // (profiles/r01_v9_plan_sweep.jsonl, r01_v10_plan_sweep.jsonl)
+            if (!rows.empty() && !tuning_knobs()) p = rows[0].plan;
+            if (rows_out) *rows_out = std::move(rows);
             if (reg_out) *reg_out = std::move(reg);
             if (dma_out) *dma_out = std::move(dma);
             return true;

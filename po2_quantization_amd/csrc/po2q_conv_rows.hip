@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "po2q_internal.h"
+#include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
 
 namespace po2q {
@@ -57,38 +58,6 @@ struct RowsArgs {
 
 constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x SW = 512 floats)
 constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
-
-// One LDS-DMA wave instruction: lane l's 16 (or 4) bytes at rsrc + voff land at
-// LDS m0 + 16*l (4*l).  `s_waitcnt lgkmcnt(0)` first: the split's reads of the slot
-// being refilled have returned.
-__device__ __forceinline__ void rows_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
-                                           uint32_t lds_addr) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %2, %3 offen lds"
-                 ::"v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
-                 : "memory");
-}
-__device__ __forceinline__ void rows_dma4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_addr) {
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen lds"
-                 ::"v"(voff), "s"(lds_addr), "s"(rs)
-                 : "memory");
-}
-// out-of-range voffset (>= the descriptor's size): the store is dropped, yet counted
-template <bool NTS = false>
-__device__ __forceinline__ void rows_store(__amdgpu_buffer_rsrc_t rs, uint32_t vo, floatx4 v) {
-    if constexpr (NTS)
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
-    else
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
-}
-template <int N>
-__device__ __forceinline__ void rows_wait() {
-    static_assert(N == 5 || N == 7, "vm ops per step: 3 DMAs + 1 or 2 stores");
-    if constexpr (N == 5)
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-}
 
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): timing ablation bits -- 1 no MFMA,
 // 2 no split (raw bits to the planes), 4 no x loads, 8 no stores.  Product: DBG = 0.
@@ -248,15 +217,11 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
             *reinterpret_cast<uint4*>(slab + a.plane + wa_i) = mid;
             *reinterpret_cast<uint4*>(slab + 2 * a.plane + wa_i) = lo;
             if (hl) {
-                const uint32_t b = *reinterpret_cast<const uint32_t*>(rw + kRawInterior + 4 * lane);
-                const float xv = __uint_as_float(b);
-                float r1 = xv - __uint_as_float(b & 0xffff0000u);
-                r1 = __builtin_isinf(xv) ? 0.0f : r1;
-                const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
-                const uint32_t lb = __float_as_uint(r1 - __uint_as_float(mb));
-                *reinterpret_cast<uint16_t*>(slab + wa_h) = (uint16_t)(b >> 16);
-                *reinterpret_cast<uint16_t*>(slab + a.plane + wa_h) = (uint16_t)(mb >> 16);
-                *reinterpret_cast<uint16_t*>(slab + 2 * a.plane + wa_h) = (uint16_t)(lb >> 16);
+                uint16_t h16, m16, l16;
+                split1(*reinterpret_cast<const uint32_t*>(rw + kRawInterior + 4 * lane), h16, m16, l16);
+                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+                *reinterpret_cast<uint16_t*>(slab + a.plane + wa_h) = m16;
+                *reinterpret_cast<uint16_t*>(slab + 2 * a.plane + wa_h) = l16;
             }
         }
         // prefetch halo row j+2 into the raw slot just split
@@ -374,8 +339,14 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
 // ------------------------------------------------------------------ planning --
 static int cdivr(int a, int b) { return (a + b - 1) / b; }
 
+// output channels across the block's waves (po2q_conv_rowsk.hip: C = K = 64)
+void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                             const float* bias, float* y, hipStream_t s);
+
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
+    rowsk_candidates(base, mode, bits, fsr, out);
     if (mode == 0 || b.groups != 1) return;
     if (bits < 1 || bits > 16) return;
     const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
@@ -448,6 +419,7 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
 
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                    const float* bias, float* y, hipStream_t s) {
+    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s);
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
     if (dbg && p.CC == 16 && p.NT == 1) {

@@ -215,9 +215,9 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
         int k, c0, tapoff;
         bool ok;
         if (pg.vr == 2) {
-            // row-streaming layout [r][ks][nt][lane][8] (po2q_conv_rows.hip), one chunk:
+            // row-streaming layout [r][ks][nt][lane][8] (po2q_conv_rows*.hip):
             //   CC = 16: ks 0 -> k < 16: s = 0, k >= 16: s = 1;  ks 1 -> k < 16: s = 2, else 0
-            //   CC = 32: ks = s, k = the 32 channels
+            //   CC = 32: ks = chunk * 3 + s, k = the chunk's 32 channels
             const int nt = t % pg.NT;
             const int ks = (t / pg.NT) % pg.ksteps;
             const int r = t / (pg.NT * pg.ksteps);
@@ -226,9 +226,9 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
             if (pg.CC == 16) {
                 sft = ks == 0 ? (grp >> 1) : (grp < 2 ? 2 : -1);
                 c0 = 8 * (grp & 1);
-            } else {
-                sft = ks;
-                c0 = 8 * grp;
+            } else {  // ks = chunk * 3 + s (po2q_conv_rowsk.hip: 2 chunks of 32 channels)
+                sft = ks % 3;
+                c0 = (ks / 3) * 32 + 8 * grp;
             }
             k = nt * 16 + (lane & 15);
             tapoff = r * 3 + sft;

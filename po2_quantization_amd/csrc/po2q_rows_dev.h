@@ -1,0 +1,71 @@
+// Device helpers shared by the row-streaming bf16x3 conv kernels
+// (po2q_conv_rows.hip, po2q_conv_rowsk.hip).  Not part of the C ABI.
+//
+// Every global access inside their row loops is inline asm, so hipcc's vmcnt
+// bookkeeping (which at a loop header falls back to vmcnt(0), i.e. waits for every
+// store and every prefetch) stays out of the picture: each step waits with one
+// exact count.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+// One LDS-DMA wave instruction: lane l's 16 (or 4) bytes at rsrc + voff land at LDS
+// m0 + 16*l (4*l).  `s_waitcnt lgkmcnt(0)` first: earlier reads of the slot being
+// refilled have returned.
+__device__ __forceinline__ void rows_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                           uint32_t lds_addr) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %0, %2, %3 offen lds"
+                 ::"v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
+                 : "memory");
+}
+__device__ __forceinline__ void rows_dma4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen lds"
+                 ::"v"(voff), "s"(lds_addr), "s"(rs)
+                 : "memory");
+}
+// out-of-range voffset (>= the descriptor's size): the store is dropped, yet counted
+template <bool NTS = false>
+__device__ __forceinline__ void rows_store(__amdgpu_buffer_rsrc_t rs, uint32_t vo, floatx4 v) {
+    if constexpr (NTS)
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
+    else
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(vo), "s"(rs));
+}
+template <int N>
+__device__ __forceinline__ void rows_wait() {
+    static_assert(N == 5 || N == 7, "vm ops per step: 3 DMAs + 1 or 2 stores");
+    if constexpr (N == 5)
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+}
+
+// Wave-uniform buffer descriptor of `bytes` (< 2^31) starting at p.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* p, int bytes) {
+    const uintptr_t bp = reinterpret_cast<uintptr_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32));
+    void* b = reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, bytes, 0x00020000);
+}
+
+// Exact 3-way split of one fp32 value (split3 of po2q_x3_dev.h, one lane value):
+// the bf16 bit patterns of hi / mid / lo.
+__device__ __forceinline__ void split1(uint32_t b, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const float xv = __uint_as_float(b);
+    float r1 = xv - __uint_as_float(b & 0xffff0000u);
+    r1 = __builtin_isinf(xv) ? 0.0f : r1;
+    const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+    const uint32_t lb = __float_as_uint(r1 - __uint_as_float(mb));
+    h = (uint16_t)(b >> 16);
+    m = (uint16_t)(mb >> 16);
+    l = (uint16_t)(lb >> 16);
+}
+
+}  // namespace po2q

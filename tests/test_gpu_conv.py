@@ -87,6 +87,9 @@ SHAPES = [
     (1, 16, 37, 68, 16, 3, 3, 1, 1, 1, 1),
     (1, 32, 23, 20, 16, 3, 3, 1, 1, 1, 1),
     (2, 32, 1, 12, 32, 3, 3, 1, 1, 1, 1),
+    # C = K = 64 (output channels across a block's waves): ragged strip, short segment
+    (2, 64, 12, 40, 64, 3, 3, 1, 1, 1, 1),
+    (1, 64, 3, 8, 64, 3, 3, 1, 1, 1, 1),
 ]
 
 
