@@ -179,7 +179,7 @@ static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
              p.nchunks, p.kblocks, p.steps, p.lds_bytes, (long long)p.blocks,
              p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4, p.dma_ov,
              p.kind == KIND_BF16X3_DMA ? (p.dma_nw > 0) : (p.nchunks > 1 || p.kblocks > 1),
-             p.kind == KIND_BF16X3 ? p.pd : 0);
+             (p.kind == KIND_BF16X3 || (p.kind == KIND_BF16X3_ROWS && p.vrx)) ? p.pd : 0);
 }
 
 int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,

@@ -39,11 +39,12 @@ __device__ __forceinline__ void rows_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
 }
 template <int N>
 __device__ __forceinline__ void rows_wait() {
-    static_assert(N == 5 || N == 7, "vm ops per step: 3 DMAs + 1 or 2 stores");
-    if constexpr (N == 5)
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    static_assert(N >= 0 && N <= 15, "vm ops issued after a row's DMAs");
+#define PO2Q_RW(n) \
+    if constexpr (N == n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory");
+    PO2Q_RW(0) PO2Q_RW(1) PO2Q_RW(2) PO2Q_RW(3) PO2Q_RW(4) PO2Q_RW(5) PO2Q_RW(6) PO2Q_RW(7)
+    PO2Q_RW(8) PO2Q_RW(9) PO2Q_RW(10) PO2Q_RW(11) PO2Q_RW(12) PO2Q_RW(13) PO2Q_RW(14) PO2Q_RW(15)
+#undef PO2Q_RW
 }
 
 // Wave-uniform buffer descriptor of `bytes` (< 2^31) starting at p.
