@@ -151,10 +151,23 @@ __device__ __forceinline__ uint16_t bf16_bits_keep_nan(float q) {
 }
 
 // W' = Q(w) / scale as bf16 bits: sign(w) * 2^e exactly (fin), else the reference's Q(w).
-__device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, int mode, int lo, int hi) {
+// thr: the mode's threshold row staged in LDS (no dependent constant-memory load per
+// weight); same decision as exponent_of (po2q_quant_dev.h).
+__device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, int mode, int lo, int hi,
+                                             const unsigned* thr) {
     if (fin) {
-        int e = 0;
-        exponent_of(wv, scale, mode, lo, hi, e);  // finite: a = |w/scale| <= 1
+        // finite scale: a = |w / scale| <= 1 (w finite; scale = max|w|)
+        const uint32_t b = __float_as_uint(wv / scale) & 0x7fffffffu;
+        int d;
+        if (b == 0u) {
+            d = lo;
+        } else if (b < 0x3f800000u) {
+            const int k = (b >= 0x00800000u) ? (int)(b >> 23) - 127 : (31 - (int)__clz(b)) - 149;
+            d = k + (b >= thr[k - PO2Q_THR_KMIN] ? 1 : 0);
+        } else {
+            d = 0;  // a == 1
+        }
+        const int e = d < lo ? lo : (d > hi ? hi : d);
         const float sg = ref_sign(wv);
         return (sg == 0.0f) ? (uint16_t)0 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
     }
@@ -171,6 +184,8 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
                                                                PackX3 pg, uint16_t* __restrict__ packed,
                                                                float* __restrict__ scale_out) {
     __shared__ unsigned red[kPackThreads / 64];
+    __shared__ unsigned thr[PO2Q_THR_COUNT];
+    for (int i = threadIdx.x; i < PO2Q_THR_COUNT; i += kPackThreads) thr[i] = po2q_thr[mode > 0 ? 1 : 0][i];
     unsigned m = 0u;
     if (nparts > 0) {
         for (int i = threadIdx.x; i < nparts; i += kPackThreads) m = max(m, partial[i]);
@@ -260,7 +275,7 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int c = c0 + e;
-            h[e] = (ok && c < pg.C) ? pack_one(w[(k * pg.C + c) * RS + tapoff], scale, fin, mode, lo, hi) : 0u;
+            h[e] = (ok && c < pg.C) ? pack_one(w[(k * pg.C + c) * RS + tapoff], scale, fin, mode, lo, hi, thr) : 0u;
         }
         out[j] = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
     }
