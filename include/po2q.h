@@ -84,6 +84,32 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
                      void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * Conv forward with its eval-mode epilogue fused into the launch:
+ *   y = act((conv(x, Q(w)) + bias) * post_scale[k] + post_shift[k] + residual)
+ * i.e. QuantizedConv2d.forward followed by the reference's eval BatchNorm (folded by
+ * the caller into post_scale = gamma / sqrt(var + eps), post_shift = beta - mean *
+ * post_scale), the residual add and the activation of its blocks:
+ *   ResNet BasicBlock   relu(bn(conv(x)) [+ shortcut])   models/resnet.py:55-71
+ *   MobileNetV2         relu6(bn(conv(x))) / bn(conv(x)) + x   models/mobilenet.py:32-33, 133-134
+ *   MobileViT           silu(bn(conv(x)))                 models/mobile_vit.py:20-21, 225-227
+ * post_scale / post_shift may be NULL (identity), residual may be NULL; residual is
+ * [N, K, P, Q] like y and must not alias y (nor may x).  act: enum po2q_act.  Same
+ * workspace as po2q_qconv2d_f32.  The row-streaming kernels apply the affine map and
+ * the activation in their store epilogue; other plans and the residual add run one
+ * extra elementwise pass over y.
+ */
+enum po2q_act { PO2Q_ACT_NONE = 0, PO2Q_ACT_RELU = 1, PO2Q_ACT_RELU6 = 2, PO2Q_ACT_SILU = 3 };
+
+int po2q_qconv2d_fused_f32(const float* x, const float* w, const float* bias, float* y,
+                           int64_t N, int64_t C, int64_t H, int64_t W,
+                           int64_t K, int64_t R, int64_t S,
+                           int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                           int64_t dil_h, int64_t dil_w, int64_t groups,
+                           int bits, int fsr, int mode, int flags,
+                           const float* post_scale, const float* post_shift, const float* residual, int act,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * Kernel autotuning, the counterpart of the reference's
  * torch.backends.cudnn.benchmark = True (train.py:33, test.py:31): times every
  * candidate plan for this problem on these buffers (synchronises the stream;

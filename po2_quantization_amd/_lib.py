@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("PO2Q_LIB", os.path.join(_HERE, "lib", "libpo2q.so"))
 
 MODES = {None: 0, "none": 0, "po2": 1, "po2+": 2}
 PRECISIONS = {"auto": 0, "fp32": 1, "bf16x3": 2}
+# fused epilogue activations (include/po2q.h enum po2q_act)
+ACTS = {None: 0, "none": 0, "relu": 1, "relu6": 2, "silu": 3}
 
 # every symbol include/po2q.h declares (checked by tests/test_capi.py)
 EXPORTS = (
@@ -25,6 +27,7 @@ EXPORTS = (
     "po2q_quantize_f32",
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
+    "po2q_qconv2d_fused_f32",
     "po2q_qconv2d_autotune",
     "po2q_qconv2d_plans",
     "po2q_qconv2d_f32_plan",
@@ -73,6 +76,8 @@ def load():
     L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32, i32, i32]
     L.po2q_qconv2d_f32.restype = i32
     L.po2q_qconv2d_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+    L.po2q_qconv2d_fused_f32.restype = i32
+    L.po2q_qconv2d_fused_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, p, p, i32, p, sz, p]
     L.po2q_qconv2d_autotune.restype = i32
     L.po2q_qconv2d_autotune.argtypes = ([p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
                                         + [ctypes.c_char_p, sz])
@@ -130,12 +135,9 @@ def _pair(v):
     return (int(v), int(v)) if isinstance(v, int) else (int(v[0]), int(v[1]))
 
 
-def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
-            precision="auto", plan=None):
-    """Fused quantize + conv forward (models/quantized_conv.py:32-38); NCHW fp32 in/out.
-
-    plan=None runs the tuned (or heuristic) plan, autotuning first when benchmark
-    mode is on; plan=i runs candidate i of plans() (tests / tuning tools)."""
+def _conv_geometry(x, w, bias, stride, padding, dilation, groups):
+    """Validate a conv call like torch's F.conv2d; returns (x, w, bias) contiguous,
+    the 14 geometry arguments of the C ABI and the output size."""
     _require_hip_f32(x, "input")
     _require_hip_f32(w, "weight")
     if bias is not None:
@@ -144,7 +146,6 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
         raise Po2qError("po2q: expected 4-D input and weight, got %d-D and %d-D" % (x.dim(), w.dim()))
     if x.device != w.device or (bias is not None and bias.device != x.device):
         raise Po2qError("po2q: input, weight and bias must be on the same device")
-    L = load()
     N, C, H, W = x.shape
     K, Cg, R, S = w.shape
     if Cg * groups != C:
@@ -156,16 +157,25 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
     P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
     Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
     args = (N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, int(groups))
+    bc = bias.contiguous() if bias is not None else None
+    return x.contiguous(), w.contiguous(), bc, args, (N, K, max(P, 0), max(Q, 0))
+
+
+def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+            precision="auto", plan=None):
+    """Fused quantize + conv forward (models/quantized_conv.py:32-38); NCHW fp32 in/out.
+
+    plan=None runs the tuned (or heuristic) plan, autotuning first when benchmark
+    mode is on; plan=i runs candidate i of plans() (tests / tuning tools)."""
+    xc, wc, bc, args, yshape = _conv_geometry(x, w, bias, stride, padding, dilation, groups)
+    L = load()
     mode_id = MODES[mode]
     prec = PRECISIONS[precision]
-    xc = x.contiguous()
-    wc = w.contiguous()
-    bc = bias.contiguous() if bias is not None else None
     with torch.cuda.device(xc.device):
         nbytes = L.po2q_qconv2d_workspace_bytes(*args, int(bits), int(fsr), mode_id, prec)
         if nbytes == 0:
             _check(1)
-        y = torch.empty((N, K, max(P, 0), max(Q, 0)), dtype=torch.float32, device=xc.device)
+        y = torch.empty(yshape, dtype=torch.float32, device=xc.device)
         ws = _workspace(nbytes, xc.device)
         bp = bc.data_ptr() if bc is not None else None
         key = args + (int(bits), int(fsr), mode_id, prec)
@@ -184,6 +194,47 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
         else:
             _check(L.po2q_qconv2d_f32(xc.data_ptr(), wc.data_ptr(), bp, y.data_ptr(), *key,
                                       ws.data_ptr(), ws.numel(), _stream(xc.device)))
+    return y
+
+
+def qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+                  precision="auto", post_scale=None, post_shift=None, residual=None, act="none"):
+    """Quantize + conv + eval epilogue in one native call (po2q_qconv2d_fused_f32):
+        y = act((conv(x, Q(w)) + bias) * post_scale[k] + post_shift[k] + residual)
+    post_scale / post_shift: [K] (an eval BatchNorm folded by the caller) or None;
+    residual: a tensor of y's shape or None; act: "none" | "relu" | "relu6" | "silu"."""
+    xc, wc, bc, args, yshape = _conv_geometry(x, w, bias, stride, padding, dilation, groups)
+    L = load()
+    mode_id = MODES[mode]
+    prec = PRECISIONS[precision]
+    ext = []
+    for t, what in ((post_scale, "post_scale"), (post_shift, "post_shift")):
+        if t is not None:
+            _require_hip_f32(t, what)
+            if t.numel() != yshape[1]:
+                raise Po2qError("po2q: %s must have %d elements, got %d" % (what, yshape[1], t.numel()))
+            t = t.contiguous()
+        ext.append(t)
+    rc = None
+    if residual is not None:
+        _require_hip_f32(residual, "residual")
+        if tuple(residual.shape) != tuple(yshape):
+            raise Po2qError("po2q: residual shape %s does not match the output %s"
+                            % (list(residual.shape), list(yshape)))
+        rc = residual.contiguous()
+    with torch.cuda.device(xc.device):
+        key = args + (int(bits), int(fsr), mode_id, prec)
+        nbytes = L.po2q_qconv2d_workspace_bytes(*key)
+        if nbytes == 0:
+            _check(1)
+        if key not in _tuned and _saved_plan(key) is None and _benchmark_enabled():
+            qconv2d(xc, wc, bc, stride, padding, dilation, groups, bits, mode, fsr, precision)  # autotune once
+        y = torch.empty(yshape, dtype=torch.float32, device=xc.device)
+        ws = _workspace(nbytes, xc.device)
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        _check(L.po2q_qconv2d_fused_f32(xc.data_ptr(), wc.data_ptr(), ptr(bc), y.data_ptr(), *key,
+                                        ptr(ext[0]), ptr(ext[1]), ptr(rc), ACTS[act],
+                                        ws.data_ptr(), ws.numel(), _stream(xc.device)))
     return y
 
 

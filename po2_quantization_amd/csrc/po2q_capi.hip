@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/po2q.h"
+#include "po2q_epi.h"
 #include "po2q_internal.h"
 
 namespace po2q {
@@ -130,9 +131,11 @@ static int check_conv_args(const float* x, const float* w, float* y, void* works
     return PO2Q_OK;
 }
 
-// Enqueue the fused quantize(+pack) and conv of plan p on stream s.
+// Enqueue the fused quantize(+pack) and conv of plan p on stream s (+ the epilogue e:
+// in the row kernels' store epilogue where they support it, else one elementwise pass).
 static int run_plan(const ConvPlan& p, const float* x, const float* w, const float* bias, float* y, int bits, int fsr,
-                    int mode, void* workspace, size_t workspace_bytes, hipStream_t s) {
+                    int mode, void* workspace, size_t workspace_bytes, hipStream_t s,
+                    const ConvEpi& e = ConvEpi{nullptr, nullptr, nullptr, 0}) {
     const WsLayout L = ws_layout(p, mode);
     if (workspace_bytes < L.total) {
         set_error("po2q: conv workspace too small (need " + std::to_string(L.total) + " bytes)");
@@ -154,19 +157,29 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
                         "weight pack launch");
         if (st) return st;
         const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
-        hipError_t e;
-        if (p.kind == KIND_BF16X3_DMA)
-            e = launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s);
-        else if (p.kind == KIND_BF16X3_ROWS)
-            e = launch_conv_bf16x3_rows(p, x, pk, scale, bias, y, s);
-        else
-            e = launch_conv_bf16x3(p, x, pk, scale, bias, y, s);
-        return hip_status(e, "conv launch");
+        hipError_t he;
+        bool fused_affine = false;
+        if (p.kind == KIND_BF16X3_DMA) {
+            he = launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s);
+        } else if (p.kind == KIND_BF16X3_ROWS && e.any()) {
+            // affine (+ activation unless a residual must be added first) in the kernel
+            he = launch_conv_bf16x3_rows_epi(p, x, pk, scale, bias, y, e.ps, e.pb, e.res ? 0 : e.act, s);
+            fused_affine = true;
+        } else if (p.kind == KIND_BF16X3_ROWS) {
+            he = launch_conv_bf16x3_rows(p, x, pk, scale, bias, y, s);
+        } else {
+            he = launch_conv_bf16x3(p, x, pk, scale, bias, y, s);
+        }
+        st = hip_status(he, "conv launch");
+        if (st || !e.any() || (fused_affine && !e.res)) return st;
+        return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, fused_affine, s), "epilogue launch");
     }
     st = hip_status(launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
                     "weight pack launch");
     if (st) return st;
-    return hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
+    st = hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
+    if (st || !e.any()) return st;
+    return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, false, s), "epilogue launch");
 }
 
 static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows"};
@@ -194,6 +207,26 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
         return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
     return run_plan(p, x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes,
                     reinterpret_cast<hipStream_t>(stream));
+}
+
+int po2q_qconv2d_fused_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
+                           int64_t H, int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w,
+                           int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits,
+                           int fsr, int mode, int flags, const float* post_scale, const float* post_shift,
+                           const float* residual, int act, void* workspace, size_t workspace_bytes, void* stream) {
+    int st = check_conv_args(x, w, y, workspace, mode, bits, flags);
+    if (st) return st;
+    if (act < PO2Q_ACT_NONE || act > PO2Q_ACT_SILU) {
+        set_error("po2q: unknown activation " + std::to_string(act));
+        return PO2Q_ERR_INVALID;
+    }
+    ConvPlan p;
+    if (!make_plan(p, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits, fsr,
+                   flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    const ConvEpi e{post_scale, post_shift, residual, act};
+    return run_plan(p, x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream), e);
 }
 
 int po2q_qconv2d_autotune(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,

@@ -41,6 +41,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "po2q_epi.h"
 #include "po2q_internal.h"
 #include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
@@ -54,6 +55,9 @@ struct RowsArgs {
     int slab;      // bytes per wave slab: 3 planes + 2 raw slots
     int w_bytes;   // weight fragment bytes at the start of LDS
     int remap;     // XCD-aware block order (gridDim.x % 8 == 0)
+    const float* ps;  // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
+    const float* pb;
+    int act;
 };
 
 constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x SW = 512 floats)
@@ -61,7 +65,7 @@ constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
 
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): timing ablation bits -- 1 no MFMA,
 // 2 no split (raw bits to the planes), 4 no x loads, 8 no stores.  Product: DBG = 0.
-template <int CC, int NT, int DBG = 0>
+template <int CC, int NT, int DBG = 0, bool EPI = false>
 __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const float* __restrict__ x,
                                                                      const uint4* __restrict__ wpk,
                                                                      const float* __restrict__ scale_p,
@@ -90,10 +94,25 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
         bk[nt] = bias ? bias[k] : 0.0f;
     }
     const float scale = *scale_p;
+    float eps_[NT], epb_[NT];  // fused epilogue: per-lane channel affine
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int k = nt * 16 + (lane & 15);
+        eps_[nt] = (EPI && a.ps) ? a.ps[k] : 1.0f;
+        epb_[nt] = (EPI && a.pb) ? a.pb[k] : 0.0f;
+    }
     // the bias loads land here (tied), not at their first use inside the row loop,
     // where hipcc would otherwise wait for vmcnt(0) -- every prefetch and store
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk[nt]));
+    for (int nt = 0; nt < NT; ++nt) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk[nt]), "+v"(eps_[nt]), "+v"(epb_[nt]));
+    // scaled accumulator -> output value (+ fused eval-BN affine and activation)
+    auto outv = [&](float accv, int nt) __attribute__((always_inline)) {
+        const float v = accv * scale + bk[nt];
+        if constexpr (EPI)
+            return epi_act(v * eps_[nt] + epb_[nt], a.act);
+        else
+            return v;
+    };
     __syncthreads();
 
     // XCD-aware block order: dispatch puts block b on XCD b % 8; the blocks one XCD
@@ -272,10 +291,10 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
 #pragma unroll
                 for (int grp = 0; grp < NG; ++grp) {
                     floatx4 v;
-                    v[0] = acc[D][grp][nt][0] * scale + bk[nt];
-                    v[1] = acc[D][grp][nt][1] * scale + bk[nt];
-                    v[2] = acc[D][grp][nt][2] * scale + bk[nt];
-                    v[3] = acc[D][grp][nt][3] * scale + bk[nt];
+                    v[0] = outv(acc[D][grp][nt][0], nt);
+                    v[1] = outv(acc[D][grp][nt][1], nt);
+                    v[2] = outv(acc[D][grp][nt][2], nt);
+                    v[3] = outv(acc[D][grp][nt][3], nt);
                     *reinterpret_cast<floatx4*>(slab + ch * 128 + 16 * ((4 * grp + g) ^ (ch & 7))) = v;
                 }
 #pragma unroll
@@ -296,10 +315,10 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                 for (int grp = 0; grp < NG; ++grp) {
                     const int q = q0 + 16 * grp + 4 * (lane >> 4);
                     floatx4 v;
-                    v[0] = acc[D][grp][nt][0] * scale + bk[nt];
-                    v[1] = acc[D][grp][nt][1] * scale + bk[nt];
-                    v[2] = acc[D][grp][nt][2] * scale + bk[nt];
-                    v[3] = acc[D][grp][nt][3] * scale + bk[nt];
+                    v[0] = outv(acc[D][grp][nt][0], nt);
+                    v[1] = outv(acc[D][grp][nt][1], nt);
+                    v[2] = outv(acc[D][grp][nt][2], nt);
+                    v[3] = outv(acc[D][grp][nt][3], nt);
                     rows_store<(DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
             }
@@ -339,10 +358,11 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
 // ------------------------------------------------------------------ planning --
 static int cdivr(int a, int b) { return (a + b - 1) / b; }
 
-// output channels across the block's waves (po2q_conv_rowsk.hip: C = K = 64)
+// output channels across the block's waves (po2q_conv_rowsk.hip: C = K in {32, 64})
 void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
 hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
-                             const float* bias, float* y, hipStream_t s);
+                             const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
+                             int act, bool epi);
 
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
@@ -401,9 +421,10 @@ void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vec
     }
 }
 
-template <int CC, int NT, int DBG = 0>
+template <int CC, int NT, int DBG = 0, bool EPI = false>
 static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
-                                const float* bias, float* y, hipStream_t s) {
+                                const float* bias, float* y, hipStream_t s, const float* ps = nullptr,
+                                const float* pb = nullptr, int act = 0) {
     RowsArgs a;
     a.N = p.N; a.C = p.C; a.H = p.H; a.W = p.W; a.K = p.K; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
@@ -412,14 +433,17 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
     a.slab = 3 * p.plane + 2 * kRawSlot;
     a.w_bytes = 3 * p.steps * p.NT * 1024;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((conv_rows<CC, NT, DBG>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    a.ps = ps;
+    a.pb = pb;
+    a.act = act;
+    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
 
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                    const float* bias, float* y, hipStream_t s) {
-    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s);
+    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
     if (dbg && p.CC == 16 && p.NT == 1) {
@@ -438,6 +462,20 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
     if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1>(p, x, packed, scale, bias, y, s);
     if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1>(p, x, packed, scale, bias, y, s);
     if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2>(p, x, packed, scale, bias, y, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace po2q
+
+namespace po2q {
+
+hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
+                                       const float* scale, const float* bias, float* y, const float* ps,
+                                       const float* pb, int act, hipStream_t s) {
+    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true);
+    if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
+    if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
+    if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
     return hipErrorInvalidValue;
 }
 

@@ -29,6 +29,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "po2q_epi.h"
 #include "po2q_internal.h"
 #include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
@@ -61,10 +62,13 @@ struct RowsKArgs {
     int N, H, W, P, Q;
     int RB, nseg, nstrip, items;
     int remap;
+    const float* ps;  // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
+    const float* pb;
+    int act;
 };
 
 // PD: halo rows in flight per wave (raw ring slots), 2 or 3
-template <int C, int PD>
+template <int C, int PD, bool EPI = false>
 __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -109,12 +113,21 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
             bw[r][ks] = __builtin_bit_cast(bf16x8, wpk[((r * KSC + ks) * WN + wn) * 64 + lane]);
     const int kout = 16 * wn + (lane & 15);
     float bk = bias ? bias[kout] : 0.0f;
+    float eps_ = (EPI && a.ps) ? a.ps[kout] : 1.0f;
+    float epb_ = (EPI && a.pb) ? a.pb[kout] : 0.0f;
     const float scale = *scale_p;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int ks = 0; ks < KSC; ++ks) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bw[r][ks]));
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk), "+v"(eps_), "+v"(epb_));
+    auto outv = [&](float accv) __attribute__((always_inline)) {
+        const float v = accv * scale + bk;
+        if constexpr (EPI)
+            return epi_act(v * eps_ + epb_, a.act);
+        else
+            return v;
+    };
 
     // ---- DMA: wave w, instruction i: lane l -> channel (C/4)w + 8i + (l >> 3), columns
     // 4*(l & 7) .. +3, landing at raw[c][col] (row-major, 128 B per channel); halo:
@@ -241,10 +254,10 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         for (int grp = 0; grp < NGW; ++grp) {
             const int q = q0 + 16 * (g0 + grp) + 4 * (lane >> 4);
             floatx4 v;
-            v[0] = acc[D][grp][0] * scale + bk;
-            v[1] = acc[D][grp][1] * scale + bk;
-            v[2] = acc[D][grp][2] * scale + bk;
-            v[3] = acc[D][grp][3] * scale + bk;
+            v[0] = outv(acc[D][grp][0]);
+            v[1] = outv(acc[D][grp][1]);
+            v[2] = outv(acc[D][grp][2]);
+            v[3] = outv(acc[D][grp][3]);
             rows_store(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
             acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
@@ -326,19 +339,24 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
 }
 
 hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
-                             const float* bias, float* y, hipStream_t s) {
+                             const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
+                             int act, bool epi) {
     RowsKArgs a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
     a.items = p.N * p.tilesP * p.tilesQ;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
-#define PO2Q_RK(c, d)                                                                                    \
-    if (p.C == c && p.pd == d) {                                                                          \
-        hipLaunchKernelGGL((conv_rowsk<c, d>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x, \
-                           reinterpret_cast<const uint4*>(packed), scale, bias, y, a);                     \
-        return hipGetLastError();                                                                         \
+    a.ps = ps;
+    a.pb = pb;
+    a.act = act;
+#define PO2Q_RK(c, d, e)                                                                                    \
+    if (p.C == c && p.pd == d && epi == e) {                                                                 \
+        hipLaunchKernelGGL((conv_rowsk<c, d, e>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x, \
+                           reinterpret_cast<const uint4*>(packed), scale, bias, y, a);                        \
+        return hipGetLastError();                                                                            \
     }
-    PO2Q_RK(64, 3) PO2Q_RK(64, 2) PO2Q_RK(32, 3) PO2Q_RK(32, 2)
+    PO2Q_RK(64, 3, false) PO2Q_RK(64, 2, false) PO2Q_RK(32, 3, false) PO2Q_RK(32, 2, false)
+    PO2Q_RK(64, 3, true) PO2Q_RK(64, 2, true) PO2Q_RK(32, 3, true) PO2Q_RK(32, 2, true)
 #undef PO2Q_RK
     return hipErrorInvalidValue;
 }

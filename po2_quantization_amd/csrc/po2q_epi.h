@@ -1,0 +1,39 @@
+// Fused conv epilogue (eval BatchNorm affine, residual add, activation): the
+// po2q_qconv2d_fused_f32 entry point (include/po2q.h).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "po2q_internal.h"
+
+namespace po2q {
+
+// y = act(v * ps[k] + pb[k] + res) with ps / pb / res optional (NULL).
+struct ConvEpi {
+    const float* ps;   // post_scale [K] or NULL
+    const float* pb;   // post_shift [K] or NULL
+    const float* res;  // residual [N, K, P, Q] or NULL
+    int act;           // PO2Q_ACT_*
+    bool any() const { return ps || pb || res || act != 0; }
+};
+
+// The activations of the reference's blocks (nn.ReLU, nn.ReLU6, nn.SiLU); NaN
+// propagates as in torch (comparisons, not fmin/fmax).
+__device__ __forceinline__ float epi_act(float v, int act) {
+    if (act == 1) return v < 0.0f ? 0.0f : v;                                // relu
+    if (act == 2) return v <= 0.0f ? 0.0f : (v >= 6.0f ? 6.0f : v);         // relu6 = hardtanh(0, 6)
+    if (act == 3) return v / (1.0f + expf(-v));                              // silu
+    return v;
+}
+
+// Row-streaming kernels with the affine map + activation in their store epilogue
+// (po2q_conv_rows.hip / po2q_conv_rowsk.hip); the residual is left to launch_epilogue.
+hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
+                                       const float* scale, const float* bias, float* y, const float* ps,
+                                       const float* pb, int act, hipStream_t s);
+
+// One elementwise pass over y [N, K, PQ]: y = act(y * ps[k] + pb[k] + res) (ps / pb
+// skipped when affine_done).
+hipError_t launch_epilogue(float* y, int64_t N, int64_t K, int64_t PQ, const ConvEpi& e, bool affine_done,
+                           hipStream_t s);
+
+}  // namespace po2q

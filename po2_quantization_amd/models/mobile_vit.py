@@ -26,7 +26,7 @@ from typing import Any, Callable, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .quantized_conv import QuantizedConv2d
+from .quantized_conv import QuantizedConv2d, can_fuse, fusable_sequence, run_fused_sequence
 
 
 def quantized_conv_1x1_bn(inp, oup, quantize_fn=None, bits=4):
@@ -126,6 +126,8 @@ class MV2Block(nn.Module):
         self.conv = nn.Sequential(*layers)
 
     def forward(self, x):
+        if can_fuse(*self.conv) and fusable_sequence(self.conv):
+            return run_fused_sequence(self.conv, x, residual=x if self.use_res_connect else None)
         y = self.conv(x)
         return y + x if self.use_res_connect else y
 
@@ -145,9 +147,14 @@ class MobileViTBlock(nn.Module):
         self.conv3 = quantized_conv_1x1_bn(dim, channel, **q)
         self.conv4 = quantized_conv_nxn_bn(2 * channel, channel, kernel_size, **q)
 
+    def _conv(self, seq, x):
+        if can_fuse(*seq) and fusable_sequence(seq):
+            return run_fused_sequence(seq, x)
+        return seq(x)
+
     def forward(self, x):
         y = x.clone()
-        x = self.conv2(self.conv1(x))  # local representation
+        x = self._conv(self.conv2, self._conv(self.conv1, x))  # local representation
         b, d, H, W = x.shape
         ph, pw = self.ph, self.pw
         h, w = H // ph, W // pw
@@ -156,7 +163,7 @@ class MobileViTBlock(nn.Module):
         t = self.transformer(t)  # global representation
         # "b (ph pw) (h w) d -> b d (h ph) (w pw)"
         x = t.view(b, ph, pw, h, w, d).permute(0, 5, 3, 1, 4, 2).reshape(b, d, H, W)
-        return self.conv4(torch.cat((self.conv3(x), y), 1))  # fusion
+        return self._conv(self.conv4, torch.cat((self._conv(self.conv3, x), y), 1))  # fusion
 
     def get_quantization_error(self):
         err, n = 0.0, 0

@@ -14,6 +14,13 @@ same get_quantization_error().  forward() runs the fused libpo2q path:
 Backward (QAT) keeps the reference's semantics: straight-through estimator on
 the weight (quantizers.py:34-36), conv gradients of the quantized weight.
 Inputs must be fp32 HIP tensors; there is no CPU path.
+
+Inference fusion: `fused(x, bn=, act=, residual=)` runs the conv
+together with the eval BatchNorm that follows it in the reference's blocks (folded
+into a per-channel affine), the activation and the residual add, in one native call
+(po2q_qconv2d_fused_f32).  The model graphs use it when no autograd graph is being
+built and the BatchNorms are in eval mode; otherwise they run the reference's module
+sequence unchanged.
 """
 import torch
 import torch.nn as nn
@@ -43,6 +50,38 @@ class _QConv2dFn(torch.autograd.Function):
         if bias is not None and ctx.needs_input_grad[2]:
             gb = gy.sum(dim=(0, 2, 3))
         return gx, gw, gb, None, None, None, None, None, None, None
+
+
+_ACT_NAMES = {nn.ReLU: "relu", nn.ReLU6: "relu6", nn.SiLU: "silu"}
+
+
+def act_name(m):
+    """'relu' / 'relu6' / 'silu' for the reference's activation modules, else None."""
+    return _ACT_NAMES.get(type(m))
+
+
+def fold_bn(bn):
+    """Eval BatchNorm as (post_scale, post_shift): y = x * s + t (torch batch_norm in eval:
+    (x - mean) / sqrt(var + eps) * weight + bias)."""
+    s = torch.rsqrt(bn.running_var + bn.eps)
+    if bn.affine:
+        s = s * bn.weight
+        return s, bn.bias - bn.running_mean * s
+    return s, -bn.running_mean * s
+
+
+def can_fuse(*mods):
+    """True when the inference fusion reproduces the module sequence: no autograd graph,
+    every BatchNorm in eval mode with running statistics."""
+    if torch.is_grad_enabled():
+        return False
+    for m in mods:
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            if m.training or m.running_mean is None or m.running_var is None:
+                return False
+        elif m is not None and m.training:
+            return False
+    return True
 
 
 class QuantizedConv2d(nn.Conv2d):
@@ -99,6 +138,22 @@ class QuantizedConv2d(nn.Conv2d):
         quantized_weight = self.quantize_fn.apply(self.weight, self.bits)
         return self._native(input, quantized_weight, "none")
 
+    def fused(self, input, bn=None, act=None, residual=None):
+        """act(bn(self(input)) + residual) in one native call (eval, no autograd; see
+        can_fuse).  bn: the following eval BatchNorm or None; act: None | 'relu' |
+        'relu6' | 'silu'."""
+        if self.padding_mode != "zeros":
+            raise RuntimeError("po2q: only padding_mode='zeros' is supported (the reference uses the default)")
+        mode = "none" if self.quantize_fn is None else NATIVE_MODES.get(self.quantize_fn)
+        weight = self.weight
+        if mode is None:  # a non-native quantizer (lin / lin+ / user Function): quantize first
+            weight = self.quantize_fn.apply(self.weight, self.bits)
+            mode = "none"
+        ps, pb = fold_bn(bn) if bn is not None else (None, None)
+        return _lib.qconv2d_fused(input, weight, self.bias, self.stride, self._padding(input), self.dilation,
+                                  self.groups, self.bits, mode, 1, self.precision, post_scale=ps, post_shift=pb,
+                                  residual=residual, act=act or "none")
+
     def get_quantization_error(self):
         # reference quantized_conv.py:40-45
         if self.quantize_fn is not None:
@@ -107,3 +162,40 @@ class QuantizedConv2d(nn.Conv2d):
         else:
             return 0, self.weight.numel()
 
+
+
+def fusable_sequence(seq):
+    """True when seq is (QuantizedConv2d, BatchNorm[, activation])* -- the conv blocks of
+    the reference's models (mobilenet.py:53-131, mobile_vit.py:15-39, 131-233)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        if not isinstance(mods[i], QuantizedConv2d):
+            return False
+        i += 1
+        if i < len(mods) and isinstance(mods[i], nn.modules.batchnorm._BatchNorm):
+            i += 1
+        if i < len(mods) and act_name(mods[i]) is not None:
+            i += 1
+    return True
+
+
+def run_fused_sequence(seq, x, residual=None):
+    """seq(x) (+ residual) with every (conv, BN, activation) group as one fused native
+    call; the residual is added by the last group, after its BN and before its
+    activation (the reference adds it after a BN-terminated group: mobilenet.py:133-134,
+    mobile_vit.py:229-230)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        conv = mods[i]
+        i += 1
+        bn = None
+        if i < len(mods) and isinstance(mods[i], nn.modules.batchnorm._BatchNorm):
+            bn = mods[i]
+            i += 1
+        act = act_name(mods[i]) if i < len(mods) else None
+        if act is not None:
+            i += 1
+        x = conv.fused(x, bn=bn, act=act, residual=residual if i >= len(mods) else None)
+    return x

@@ -17,7 +17,7 @@ from typing import Callable, Optional
 import torch
 import torch.nn as nn
 
-from .quantized_conv import QuantizedConv2d
+from .quantized_conv import QuantizedConv2d, can_fuse, run_fused_sequence
 
 
 class BasicBlock(nn.Module):
@@ -35,6 +35,11 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if can_fuse(self.bn1, self.bn2, self.downsample):
+            # inference: conv+BN+ReLU and conv+BN+add+ReLU as single native calls
+            shortcut = x if self.downsample is None else run_fused_sequence(self.downsample, x)
+            out = self.conv1.fused(x, bn=self.bn1, act="relu")
+            return self.conv2.fused(out, bn=self.bn2, residual=shortcut, act="relu")
         shortcut = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))

@@ -241,3 +241,64 @@ def test_weight_special_values():
     w = torch.randn(4, 4, 3, 3, device=DEV)
     w[0, 0, 0, 0] = float("nan")
     assert torch.isnan(_lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, "po2+")).all()
+
+
+FUSED_SHAPES = [  # (N, C, H, W, K, R, stride, pad, groups): row kernels, K-split, tile, depthwise, 1x1
+    (2, 16, 40, 36, 16, 3, 1, 1, 1),
+    (2, 32, 20, 24, 32, 3, 1, 1, 1),
+    (1, 64, 12, 40, 64, 3, 1, 1, 1),
+    (2, 16, 33, 31, 32, 3, 2, 1, 1),
+    (2, 32, 16, 16, 64, 1, 2, 0, 1),
+    (2, 96, 9, 9, 96, 3, 1, 1, 96),
+]
+
+
+@pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[str(s) for s in FUSED_SHAPES])
+@pytest.mark.parametrize("act", ["none", "relu", "relu6", "silu"])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_fused_epilogue_vs_torch(shape, act, with_res):
+    """po2q_qconv2d_fused_f32 == act(bn_eval(F.conv2d(x, Q(w))) + residual) in torch fp32
+    (the reference's block order, resnet.py:55-71 / mobilenet.py:32-33 / mobile_vit.py:20-21)."""
+    N, C, H, W, K, R, st, pad, groups = shape
+    g = torch.Generator().manual_seed(hash((shape, act, with_res)) & 0xFFFF)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    w = (torch.randn(K, C // groups, R, R, generator=g) * 0.2).to(DEV)
+    bn = torch.nn.BatchNorm2d(K).to(DEV).eval()
+    with torch.no_grad():
+        bn.weight.copy_(1.0 + 0.2 * torch.randn(K, generator=g))
+        bn.bias.copy_(0.1 * torch.randn(K, generator=g))
+        bn.running_mean.copy_(0.1 * torch.randn(K, generator=g))
+        bn.running_var.copy_(torch.rand(K, generator=g) + 0.5)
+    from po2_quantization_amd.models.quantized_conv import fold_bn
+
+    acts = {"none": lambda t: t, "relu": torch.relu, "relu6": torch.nn.functional.relu6,
+            "silu": torch.nn.functional.silu}
+    with torch.no_grad():
+        qw = _lib.quantize(w, 4, "po2")
+        y0 = bn(torch.nn.functional.conv2d(x, qw, None, st, pad, 1, groups))
+        res = torch.randn(y0.shape, generator=g).to(DEV) if with_res else None
+        ref = acts[act](y0 + res if with_res else y0)
+        ps, pb = fold_bn(bn)
+        y = _lib.qconv2d_fused(x, w, None, st, pad, 1, groups, 4, "po2", post_scale=ps, post_shift=pb,
+                               residual=res, act=act)
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    assert err <= CONV_TOL, err
+
+
+def test_fused_every_row_plan_and_rejects_bad_act():
+    """Every candidate plan of a row-kernel shape gives the same fused result (the tuned
+    plan is the one the fused entry runs); an unknown activation raises."""
+    N, C, H, W, K = 1, 32, 16, 32, 32
+    torch.manual_seed(3)
+    x = torch.randn(N, C, H, W, device=DEV)
+    w = torch.randn(K, C, 3, 3, device=DEV) * 0.1
+    ps = torch.rand(K, device=DEV) + 0.5
+    pb = torch.randn(K, device=DEV) * 0.1
+    ref = torch.relu(_lib.qconv2d(x, w, None, 1, 1) * ps.view(1, -1, 1, 1) + pb.view(1, -1, 1, 1))
+    y = _lib.qconv2d_fused(x, w, None, 1, 1, post_scale=ps, post_shift=pb, act="relu")
+    assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL
+    L = _lib.load()
+    with pytest.raises(_lib.Po2qError, match="activation"):
+        _lib._check(L.po2q_qconv2d_fused_f32(x.data_ptr(), w.data_ptr(), None, y.data_ptr(), N, C, H, W, K, 3, 3,
+                                             1, 1, 1, 1, 1, 1, 1, 4, 1, 1, 0, None, None, None, 9,
+                                             x.data_ptr(), 1 << 20, None))

@@ -34,10 +34,27 @@ def _cpu_qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bit
     return torch.nn.functional.conv2d(x, qw, bias, stride, padding, dilation, groups)
 
 
+_ACTS = {"none": lambda t: t, "relu": torch.relu, "relu6": lambda t: torch.clamp(t, 0.0, 6.0),
+         "silu": torch.nn.functional.silu}
+
+
+def _cpu_qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+                       precision="auto", post_scale=None, post_shift=None, residual=None, act="none"):
+    y = _cpu_qconv2d(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr)
+    if post_scale is not None:
+        y = y * post_scale.view(1, -1, 1, 1)
+    if post_shift is not None:
+        y = y + post_shift.view(1, -1, 1, 1)
+    if residual is not None:
+        y = y + residual
+    return _ACTS[act](y)
+
+
 @pytest.fixture
 def cpu_double(monkeypatch):
     monkeypatch.setattr(_lib, "quantize", _cpu_quantize)
     monkeypatch.setattr(_lib, "qconv2d", _cpu_qconv2d)
+    monkeypatch.setattr(_lib, "qconv2d_fused", _cpu_qconv2d_fused)
 
 
 MODELS = [("resnet20", None, 4), ("resnet56", "po2", 4), ("resnet20", "po2+", 3), ("mobilenet", "po2+", 4),
