@@ -446,6 +446,16 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
+    if (dbg && p.CC == 32 && p.NT == 2) {
+        switch (atoi(dbg)) {
+#define PO2Q_ROWS_CASE(d) \
+    case d: return launch_rows_t<32, 2, d>(p, x, packed, scale, bias, y, s);
+            PO2Q_ROWS_CASE(1) PO2Q_ROWS_CASE(2) PO2Q_ROWS_CASE(4) PO2Q_ROWS_CASE(8) PO2Q_ROWS_CASE(12)
+            PO2Q_ROWS_CASE(3) PO2Q_ROWS_CASE(14)
+#undef PO2Q_ROWS_CASE
+            default: break;
+        }
+    }
     if (dbg && p.CC == 16 && p.NT == 1) {
         switch (atoi(dbg)) {
 #define PO2Q_ROWS_CASE(d) \

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -68,7 +69,9 @@ struct RowsKArgs {
 };
 
 // PD: halo rows in flight per wave (raw ring slots), 2 or 3
-template <int C, int PD, bool EPI = false>
+// DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): 1 = halo-column DMAs read nothing
+// (out-of-range offsets; timing only, outputs wrong).  Product builds: DBG = 0.
+template <int C, int PD, bool EPI = false, int DBG = 0>
 __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         const uint32_t base = raw_lds + (uint32_t)(sl * RAWS);
 #pragma unroll
         for (int i = 0; i < DPW; ++i) rows_dma16(rs, vo, i * soff1, base + (uint32_t)(DPW * wave + i) * 1024u);
-        const uint32_t voh = (hok && qh_ok) ? vh0 + roff : 0x7fffffffu;
+        const uint32_t voh = (hok && qh_ok && !(DBG & 1)) ? vh0 + roff : 0x7fffffffu;
         rows_dma4(rs, voh, base + (uint32_t)RAWI + (uint32_t)wave * 256u);
     };
     // vm ops issued after a row's DMAs (step j-PD) until row j is split: that step's
@@ -355,8 +358,23 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
                            reinterpret_cast<const uint4*>(packed), scale, bias, y, a);                        \
         return hipGetLastError();                                                                            \
     }
+#ifdef PO2Q_ROWS_DIAG
+    if (getenv("PO2Q_ROWSK_DEBUG") && atoi(getenv("PO2Q_ROWSK_DEBUG")) == 1) {
+        if (p.C == 64 && p.pd == 3) {
+            hipLaunchKernelGGL((conv_rowsk<64, 3, false, 1>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes,
+                               s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+            return hipGetLastError();
+        }
+        if (p.C == 32 && p.pd == 2) {
+            hipLaunchKernelGGL((conv_rowsk<32, 2, false, 1>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes,
+                               s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+            return hipGetLastError();
+        }
+    }
+#endif
     PO2Q_RK(64, 3, false) PO2Q_RK(64, 2, false) PO2Q_RK(32, 3, false) PO2Q_RK(32, 2, false)
     PO2Q_RK(64, 3, true) PO2Q_RK(64, 2, true) PO2Q_RK(32, 3, true) PO2Q_RK(32, 2, true)
+
 #undef PO2Q_RK
     return hipErrorInvalidValue;
 }

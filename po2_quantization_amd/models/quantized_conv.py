@@ -70,10 +70,14 @@ def fold_bn(bn):
     return s, -bn.running_mean * s
 
 
+# Inference fusion switch (tools/model_bench.py times both sides).
+INFERENCE_FUSION = True
+
+
 def can_fuse(*mods):
     """True when the inference fusion reproduces the module sequence: no autograd graph,
     every BatchNorm in eval mode with running statistics."""
-    if torch.is_grad_enabled():
+    if not INFERENCE_FUSION or torch.is_grad_enabled():
         return False
     for m in mods:
         if isinstance(m, nn.modules.batchnorm._BatchNorm):
