@@ -44,7 +44,9 @@ constexpr int kKWC = kKSW + 2;                 // halo columns
 template <int C> constexpr int kKPlane = kKWC * C * 2;          // bytes per bf16 plane
 template <int C> constexpr int kKRawInt = C * kKSW * 4;        // raw interior [C][32] fp32
 template <int C> constexpr int kKRawSlot = kKRawInt<C> + 4 * 256;  // + 4 waves x 64 halo dwords
-template <int C, int PD> constexpr int kKLds = 2 * 3 * kKPlane<C> + PD * kKRawSlot<C>;
+template <int C> constexpr int kKTile = C * kKSW * 4;           // output row tile [K][32] fp32
+template <int C, int PD, bool TT>
+constexpr int kKLds = 2 * 3 * kKPlane<C> + PD * kKRawSlot<C> + (TT ? 2 * kKTile<C> : 0);
 
 // byte offset of (halo column hc, channel octet oct) in a plane, 2C bytes per pixel;
 // octets XOR-swizzled by the column (C = 64: 8 octets, C = 32: the x_addr<32> layout)
@@ -68,11 +70,73 @@ struct RowsKArgs {
     int act;
 };
 
-// PD: halo rows in flight per wave (raw ring slots), 2 or 3
-// DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): 1 = halo-column DMAs read nothing
-// (out-of-range offsets; timing only, outputs wrong).  Product builds: DBG = 0.
-template <int C, int PD, bool EPI = false, int DBG = 0>
-__global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
+// The LW loader wave: every DMA of the block, the layout the MFMA waves' own DMAs
+// would have produced (interior: instruction i, lane l -> channel 8i + (l >> 3),
+// columns 4(l & 7) .. +3 at raw[c][col]; halo: lane l -> side l / C, channel l % C).
+// Row j is published by the barrier of step j - 1 (barrier -1: the preamble's), and
+// its slot is refilled with row j + PD after the barrier of step j, so it executes
+// exactly the MFMA waves' barriers: one preamble, one per (whole-triple) step and the
+// TT flush.
+template <int C, int PD, bool TT>
+__device__ __forceinline__ void loader_wave(const float* __restrict__ x, const RowsKArgs& a, unsigned char* raw,
+                                            int n, int q0, int p0, int nrows) {
+    constexpr int NI = C / 8 + 1;  // instructions per row: C/8 interior + 1 halo
+    static_assert(2 * C <= 64, "one halo instruction per row");
+    const int lane = threadIdx.x & 63;
+    const int HW = a.H * a.W;
+    const uint32_t cstride = (uint32_t)HW * 4u;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * C * HW, C * HW * 4);
+    const int gq4 = q0 + 4 * (lane & 7);
+    const bool qi_ok = gq4 < a.W;
+    const uint32_t vi0 = (uint32_t)(lane >> 3) * cstride + (uint32_t)gq4 * 4u;
+    const int hside = lane / C, hch = lane % C;
+    const int gqh = hside ? q0 + kKSW : q0 - 1;
+    const bool qh_ok = gqh >= 0 && gqh < a.W;
+    const uint32_t vh0 = (uint32_t)hch * cstride + (uint32_t)gqh * 4u;
+    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    auto lrow = [&](int sl, int j) __attribute__((always_inline)) {
+        const int h = p0 - 1 + j;
+        const bool hok = j < nrows && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t vo = (hok && qi_ok) ? vi0 + roff : 0x7fffffffu;
+        const uint32_t base = raw_lds + (uint32_t)(sl * kKRawSlot<C>);
+#pragma unroll
+        for (int i = 0; i < C / 8; ++i) rows_dma16(rs, vo, i * 8u * cstride, base + (uint32_t)i * 1024u);
+        rows_dma4(rs, (hok && qh_ok) ? vh0 + roff : 0x7fffffffu, base + (uint32_t)kKRawInt<C>);
+    };
+#pragma unroll
+    for (int r = 0; r < PD; ++r) lrow(r, r);
+    rows_wait<(PD - 1) * NI>();  // row 0
+    __builtin_amdgcn_s_barrier();
+    const int steps = (nrows + 2) / 3 * 3;  // the MFMA waves run whole triples of steps
+    int sl = 0;
+    for (int j = 0; j < steps; ++j) {
+        rows_wait<(PD - 2) * NI>();  // row j + 1 (issued after it: rows j + 2 .. j + PD - 1)
+        __builtin_amdgcn_s_barrier();
+        lrow(sl, j + PD);  // the slot of row j, split before this barrier
+        sl = sl + 1 == PD ? 0 : sl + 1;
+    }
+    if (TT && nrows % 3 == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// PD: halo rows in flight per wave (raw ring slots): 2 or 3 (a divisor of the 6-step
+//     unroll)
+// TT: output rows leave through a double-buffered LDS tile [K][32 columns]: a row
+//     completed in step j is stored in step j+1 as 128-byte channel runs (8 channels
+//     per wave instruction) instead of one 64-byte run per channel and column group
+// LW: a fifth, loader wave issues every DMA of the block (and joins the per-row
+//     barrier); the four MFMA waves issue no global loads, only stores.  A wave's
+//     loads queue behind its own earlier stores, so a wave that both streams stores
+//     and loads gets about half the store rate of a store-only wave (r01_v13 ablation)
+// DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG; timing only, outputs wrong): bit 1 =
+// halo-column DMAs read nothing, 2 = no MFMAs, 4 = no split, 8 = interior DMAs read
+// nothing, 16 = stores write nothing (dropped instructions still issue and count),
+// 32 = TT stores non-temporal, 64 = no wait for the DMAs (vmcnt 31), 128 = no DMA
+// instructions in the loop, 256 = no TT tile LDS traffic.
+// Product builds: DBG = 0.
+template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0>
+__global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
                                                           RowsKArgs a) {
@@ -93,6 +157,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
     const int g0 = (wave / WN) * NGW;            // first column group of this wave
     unsigned char* planes = lds;                 // 2 buffers x 3 planes
     unsigned char* raw = lds + 2 * 3 * PL;       // PD slots
+    unsigned char* tile = raw + PD * kKRawSlot<C>;  // TT: 2 output row tiles
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -106,6 +171,13 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
     const int p0 = seg * a.RB;
     const int rbe = min(a.RB, a.P - p0);
     const int nrows = rbe + 2;
+
+    if constexpr (LW) {
+        if (wave == 4) {
+            loader_wave<C, PD, TT>(x, a, raw, n, q0, p0, nrows);
+            return;
+        }
+    }
 
     // ---- this wave's weights: B[r][ks = chunk*3 + s] for output channels 16w..16w+15
     bf16x8 bw[3][KSC];
@@ -172,15 +244,16 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
                     aoff[grp][ch * 3 + s] = k_addr<C>(16 * (g0 + grp) + p + s, 4 * ch + g);
     }
 
-    auto load_row = [&](int sl, int j) __attribute__((always_inline)) {
+    auto load_row = [&](auto SL_, int j) __attribute__((always_inline)) {
+        constexpr int sl = decltype(SL_)::value;
         const int h = p0 - 1 + j;
         const bool hok = j < nrows && h >= 0 && h < a.H;
         const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
-        const uint32_t vo = (hok && qi_ok) ? vi0 + roff : 0x7fffffffu;
+        const uint32_t vo = (hok && qi_ok && !(DBG & 8)) ? vi0 + roff : 0x7fffffffu;
+        const uint32_t voh = (hok && qh_ok && !(DBG & 1)) ? vh0 + roff : 0x7fffffffu;
         const uint32_t base = raw_lds + (uint32_t)(sl * RAWS);
 #pragma unroll
         for (int i = 0; i < DPW; ++i) rows_dma16(rs, vo, i * soff1, base + (uint32_t)(DPW * wave + i) * 1024u);
-        const uint32_t voh = (hok && qh_ok && !(DBG & 1)) ? vh0 + roff : 0x7fffffffu;
         rows_dma4(rs, voh, base + (uint32_t)RAWI + (uint32_t)wave * 256u);
     };
     // vm ops issued after a row's DMAs (step j-PD) until row j is split: that step's
@@ -188,6 +261,21 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
     constexpr int VMW = (PD - 1) * (DPW + 1 + NGW) + NGW;
     const int PQ = a.P * a.Q;
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * K * PQ, K * PQ * 4);
+
+    // TT stores: wave w, instruction i: lane l -> channel (K/4)w + 8i + (l >> 3), columns
+    // q0 + 4(l & 7) .. +3 (the tile's 16-byte blocks are XOR-swizzled by channel)
+    auto store_tile = [&](const unsigned char* tr, int o, bool orow) __attribute__((always_inline)) {
+        const int sb = lane & 7;
+        const int q = q0 + 4 * sb;
+#pragma unroll
+        for (int i = 0; i < NGW; ++i) {
+            const int c = (K / 4) * wave + 8 * i + (lane >> 3);
+            floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (!(DBG & 256)) v = *reinterpret_cast<const floatx4*>(tr + c * (kKSW * 4) + ((sb ^ (c & 7)) << 4));
+            const uint32_t vo = (uint32_t)c * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + (uint32_t)q;
+            rows_store<(DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
+        }
+    };
 
     floatx4 acc[3][NGW];
 #pragma unroll
@@ -202,8 +290,14 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         constexpr int RS = S6 % PD; // raw slot
         unsigned char* pb = planes + B2 * 3 * PL;
         const unsigned char* rw = raw + RS * RAWS;
-        rows_wait<VMW>();  // this wave's DMAs of row j have landed
-        {
+        if constexpr (LW) {
+            // (the loader published row j at the previous barrier)
+        } else if constexpr (DBG & 64) {
+            rows_wait<31>();
+        } else {
+            rows_wait<VMW>();  // this wave's DMAs of row j have landed
+        }
+        if constexpr (!(DBG & 4)) {
             uint32_t b8[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) b8[e] = *reinterpret_cast<const uint32_t*>(rw + rd0 + e * (kKSW * 4));
@@ -216,7 +310,9 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
             }
             if (lane < HPW) {
                 uint16_t h16, m16, l16;
-                split1(*reinterpret_cast<const uint32_t*>(rw + RAWI + wave * 256 + 4 * lane), h16, m16, l16);
+                // halo value hv = HPW * wave + lane: own DMA at [wave][lane], LW's at [hv]
+                const int hoff = LW ? 4 * (HPW * wave + lane) : wave * 256 + 4 * lane;
+                split1(*reinterpret_cast<const uint32_t*>(rw + RAWI + hoff), h16, m16, l16);
                 *reinterpret_cast<uint16_t*>(pb + wa_h) = h16;
                 *reinterpret_cast<uint16_t*>(pb + PL + wa_h) = m16;
                 *reinterpret_cast<uint16_t*>(pb + 2 * PL + wa_h) = l16;
@@ -227,11 +323,11 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         // refill the raw slot this wave just split (its own data only)
-        load_row(RS, j + PD);
+        if constexpr (!(DBG & 128) && !LW) load_row(std::integral_constant<int, RS>{}, j + PD);
         // MFMAs: halo row j feeds output halo-index j+1 (r=0), j (r=1), j-1 (r=2)
         constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
 #pragma unroll
-        for (int ks = 0; ks < KSC; ++ks) {
+        for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
             bf16x8 af[3][NGW];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
@@ -250,6 +346,26 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         }
         // output halo-index j-1 (row p0 + j - 2) is complete
         constexpr int D = (S + 2) % 3;
+        if constexpr (TT) {
+            // store the row completed in the previous step (tile 1 - B2, published by
+            // this step's barrier), then park this step's row in tile B2
+            // (the loop runs whole triples of steps: steps past nrows - 1 only store)
+            store_tile(tile + (1 - B2) * kKTile<C>, p0 + j - 3, j >= 3 && j - 3 < rbe);
+            unsigned char* tw = tile + B2 * kKTile<C>;
+#pragma unroll
+            for (int grp = 0; grp < NGW; ++grp) {
+                floatx4 v;
+                v[0] = outv(acc[D][grp][0]);
+                v[1] = outv(acc[D][grp][1]);
+                v[2] = outv(acc[D][grp][2]);
+                v[3] = outv(acc[D][grp][3]);
+                const int bi = 4 * (g0 + grp) + (lane >> 4);
+                if constexpr (!(DBG & 256))
+                    *reinterpret_cast<floatx4*>(tw + kout * (kKSW * 4) + ((bi ^ (kout & 7)) << 4)) = v;
+                acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+            return;
+        }
         const int o = p0 + j - 2;
         const bool orow = j >= 2 && o < p0 + rbe;
         const uint32_t yk = (uint32_t)kout * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q;
@@ -261,18 +377,24 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
             v[1] = outv(acc[D][grp][1]);
             v[2] = outv(acc[D][grp][2]);
             v[3] = outv(acc[D][grp][3]);
-            rows_store(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+            rows_store(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
             acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
     };
 
     {
         const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < PD; ++r) {
-            load_row(r, r);
+        auto pre = [&](auto R_) __attribute__((always_inline)) {
+            load_row(R_, decltype(R_)::value);
 #pragma unroll
             for (int i = 0; i < NGW; ++i) rows_store(ry, 0x7fffffffu, z);
+        };
+        if constexpr (LW) {
+            __builtin_amdgcn_s_barrier();  // the loader has rows 0 .. PD-1 in flight, row 0 landed
+        } else {
+            pre(std::integral_constant<int, 0>{});
+            pre(std::integral_constant<int, 1>{});
+            if constexpr (PD >= 3) pre(std::integral_constant<int, 2>{});
         }
     }
     for (int j = 0; j < nrows; j += 6) {
@@ -284,6 +406,13 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
         step(std::integral_constant<int, 4>{}, j + 4);
         step(std::integral_constant<int, 5>{}, j + 5);
     }
+    if (TT && nrows % 3 == 0) {
+        // the last row (parked by step nrows - 1; with nrows % 3 != 0 the loop's extra
+        // step nrows has stored it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        store_tile(tile + ((nrows - 1) & 1) * kKTile<C>, p0 + rbe - 1, true);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
 }
 
@@ -291,6 +420,14 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 3 : 4) void conv_rowsk(const fl
 // Candidates for 3x3 / s1 / p1 / C = K = 64 (plan kind bf16x3_rows with vrx = 1:
 // output channels across the block's waves).  Weight pack: the row layout
 // [r][ks = chunk*3 + s][nt][lane][8] (po2q_quant.hip, CC = 32, 2 chunks).
+static int rowsk_lds(int C, int pd, bool tt) {
+#define PO2Q_L(c, d) \
+    if (C == c && pd == d) return tt ? kKLds<c, d, true> : kKLds<c, d, false>;
+    PO2Q_L(64, 2) PO2Q_L(64, 3) PO2Q_L(32, 2) PO2Q_L(32, 3)
+#undef PO2Q_L
+    return 1 << 30;
+}
+
 void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     if (mode == 0 || b.groups != 1) return;
     if (bits < 1 || bits > 16) return;
@@ -317,27 +454,40 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
     p.plane = b.C == 64 ? kKPlane<64> : kKPlane<32>;
     p.packed_floats = (int64_t)3 * p.steps * p.NT * 64 * 4;
     p.tilesQ = (p.Q + kKSW - 1) / kKSW;
-    // blocks resident per chip: 3 per CU for C = 64 (VGPR budget), 4 for C = 32
-    const int slots = 256 * (b.C == 64 ? 3 : 4);
-    std::vector<std::pair<double, int>> rbs;
-    for (int rb = 4; rb <= p.P; ++rb) {
-        const int nseg = (p.P + rb - 1) / rb;
-        if (rb != (p.P + nseg - 1) / nseg) continue;
-        const int64_t items = (int64_t)p.N * nseg * p.tilesQ;
-        if (items > INT_MAX / 2) continue;
-        rbs.push_back({(double)((items + slots - 1) / slots) * (rb + 2), rb});
-    }
-    std::sort(rbs.begin(), rbs.end());
-    for (int pd : {3, 2})  // prefetch depth (halo rows in flight); 3 slots fit 3 blocks / CU
-        for (int i = 0; i < (int)rbs.size() && i < 3; ++i) {
+    // vrx = 2: stores through the LDS output tile (TT); pd: prefetch depth (halo rows in
+    // flight per wave)
+    // vrx: 1 = direct stores, 2 = stores through the LDS output tile (TT), 3 = TT with
+    // the loader wave (LW, C = 32); pd: rows in flight per wave
+    const int vrxs[3] = {b.C == 64 ? 1 : 3, 2, b.C == 64 ? 0 : 1};
+    for (int vrx : vrxs)
+        for (int pd : {3, 2}) {
+            if (vrx == 0 || (vrx == 3 && pd < 3)) continue;  // LW: two rows in flight at least
             ConvPlan c = p;
             c.pd = pd;
-            c.lds_bytes = b.C == 64 ? (pd == 3 ? kKLds<64, 3> : kKLds<64, 2>) : (pd == 3 ? kKLds<32, 3> : kKLds<32, 2>);
-            c.TP = rbs[i].second;
-            c.tilesP = (p.P + c.TP - 1) / c.TP;
-            const int64_t items = (int64_t)p.N * c.tilesP * c.tilesQ;
-            c.blocks = (items + 7) / 8 * 8;
-            out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), c});
+            c.vrx = vrx;
+            const bool tt = vrx >= 2;
+            c.lds_bytes = rowsk_lds(b.C, pd, tt);
+            // blocks resident per chip: VGPR budget (C = 64: 3 per CU, 2 with TT; C = 32: 4)
+            // and LDS (160 KiB per CU)
+            const int per_cu = std::min(b.C == 64 ? (tt ? 2 : 3) : 4, (int)(163840 / c.lds_bytes));
+            const int slots = 256 * per_cu;
+            std::vector<std::pair<double, int>> rbs;
+            for (int rb = 4; rb <= p.P; ++rb) {
+                const int nseg = (p.P + rb - 1) / rb;
+                if (rb != (p.P + nseg - 1) / nseg) continue;
+                const int64_t items = (int64_t)p.N * nseg * p.tilesQ;
+                if (items > INT_MAX / 2) continue;
+                rbs.push_back({(double)((items + slots - 1) / slots) * (rb + 2), rb});
+            }
+            std::sort(rbs.begin(), rbs.end());
+            for (int i = 0; i < (int)rbs.size() && i < 2; ++i) {
+                ConvPlan d = c;
+                d.TP = rbs[i].second;
+                d.tilesP = (p.P + d.TP - 1) / d.TP;
+                const int64_t items = (int64_t)p.N * d.tilesP * d.tilesQ;
+                d.blocks = (items + 7) / 8 * 8;
+                out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0) + (vrx == vrxs[0] ? 0.0 : 0.02), d});
+            }
         }
 }
 
@@ -352,30 +502,34 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     a.ps = ps;
     a.pb = pb;
     a.act = act;
-#define PO2Q_RK(c, d, e)                                                                                    \
-    if (p.C == c && p.pd == d && epi == e) {                                                                 \
-        hipLaunchKernelGGL((conv_rowsk<c, d, e>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x, \
-                           reinterpret_cast<const uint4*>(packed), scale, bias, y, a);                        \
+#define PO2Q_RK1(c, d, e, v, tt, lw)                                                                      \
+    if (p.C == c && p.pd == d && epi == e && p.vrx == v) {                                                   \
+        hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e>), dim3((unsigned)p.blocks), dim3(kThreads + (lw ? 64 : 0)), \
+                           p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);     \
         return hipGetLastError();                                                                            \
     }
+#define PO2Q_RK(c, d, e) PO2Q_RK1(c, d, e, 1, false, false) PO2Q_RK1(c, d, e, 2, true, false)
 #ifdef PO2Q_ROWS_DIAG
-    if (getenv("PO2Q_ROWSK_DEBUG") && atoi(getenv("PO2Q_ROWSK_DEBUG")) == 1) {
-        if (p.C == 64 && p.pd == 3) {
-            hipLaunchKernelGGL((conv_rowsk<64, 3, false, 1>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes,
-                               s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
-            return hipGetLastError();
-        }
-        if (p.C == 32 && p.pd == 2) {
-            hipLaunchKernelGGL((conv_rowsk<32, 2, false, 1>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes,
-                               s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
-            return hipGetLastError();
-        }
+    if (const char* dv = getenv("PO2Q_ROWSK_DEBUG")) {
+        const int dbg = atoi(dv);
+#define PO2Q_RKD(c, d, tt, lw, v)                                                                          \
+    if (dbg == v && p.C == c && p.pd == d && (p.vrx >= 2) == tt && (p.vrx == 3) == lw) {                   \
+        hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, false, v>), dim3((unsigned)p.blocks), dim3(kThreads + (lw ? 64 : 0)), \
+                           p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);    \
+        return hipGetLastError();                                                                           \
+    }
+#define PO2Q_RKDS(v) PO2Q_RKD(32, 3, true, false, v) PO2Q_RKD(32, 3, true, true, v)
+        PO2Q_RKDS(6) PO2Q_RKDS(16) PO2Q_RKDS(2) PO2Q_RKDS(1) PO2Q_RKDS(7)
+#undef PO2Q_RKDS
+#undef PO2Q_RKD
     }
 #endif
     PO2Q_RK(64, 3, false) PO2Q_RK(64, 2, false) PO2Q_RK(32, 3, false) PO2Q_RK(32, 2, false)
     PO2Q_RK(64, 3, true) PO2Q_RK(64, 2, true) PO2Q_RK(32, 3, true) PO2Q_RK(32, 2, true)
+    PO2Q_RK1(32, 3, false, 3, true, true) PO2Q_RK1(32, 3, true, 3, true, true)
 
 #undef PO2Q_RK
+#undef PO2Q_RK1
     return hipErrorInvalidValue;
 }
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--var", default="PO2Q_X3_DEBUG", help="ablation switch (PO2Q_ROWS_DEBUG for the row kernel)")
     ap.add_argument("--values", default="0,1,2,3,4,8,12,5,7,9,11,13,14,15")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved repetitions (median reported)")
     args = ap.parse_args()
     C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
     if args.tile:
@@ -33,9 +34,14 @@ def main():
     descs = _lib.plans(args.batch, C, H, H, K, R, R, st, pad)
     for pl in plans:
         res = {"plan": _lib.describe(args.batch, C, H, H, K, R, R, st, pad) if pl is None else descs[pl]}
-        for dbg in (int(v) for v in args.values.split(",")):
-            os.environ[args.var] = str(dbg)
-            res[str(dbg)] = round(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=pl), 7), 4)
+        ts = {}
+        for _ in range(args.rounds):  # interleaved, so drift between rounds hits every value alike
+            for dbg in (int(v) for v in args.values.split(",")):
+                os.environ[args.var] = str(dbg)
+                t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=pl), 7)
+                ts.setdefault(str(dbg), []).append(t)
+        for k, v in ts.items():
+            res[k] = round(sorted(v)[len(v) // 2], 4)
         os.environ.pop(args.var)
         print(json.dumps(res), flush=True)
     res = {}

@@ -34,7 +34,7 @@ def short(desc):
     f = dict(kv.split("=") for kv in desc.split())
     k = ("dma%s%s%s" % (f["waves"], "ov" if f.get("ov") == "1" else "", "" if f.get("wstream") != "0" else "wr")
          if f["kind"] == "bf16x3_dma" else ("reg" if f["kind"] == "bf16x3" else f["kind"]))
-    return "%s NJ=%s vr=%s %s" % (k, f["NJ"], f["vr"], f["tile"])
+    return "%s NJ=%s vr=%s pd=%s %s" % (k, f["NJ"], f["vr"], f.get("pd", "0"), f["tile"])
 
 
 def main():
