@@ -60,6 +60,22 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
                       void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * Linear power-of-two quantizers lin / lin+ (per input channel = dim 1 of a 4-D weight).
+ * Replaces LinearPowerOfTwoQuantizer.forward     (utils/quantizers.py:59-96)
+ *      and LinearPowerOfTwoPlusQuantizer.forward (utils/quantizers.py:99-136):
+ *   delta_c = (max_c - min_c) / (2^bits - 1), then num_iters least-squares refits of
+ *   delta_c snapped to 2 ** round(log2(.)) (lin+: of sqrt(8/9) * delta_c);
+ *   out = delta_c * clamp(round(w / delta_c), -(2^(bits-1) - 1), 2^(bits-1) - 1).
+ * w, out [d0, d1, d2, d3] fp32 contiguous (may not alias).  Elementwise steps are the
+ * reference's fp32 operations; the two refit sums are fp64 (deterministic).  A constant
+ * channel (delta 0) or a NaN gives NaN, as in the reference.  Every d > 0 (the
+ * reference's torch.max(dim) raises on an empty dim), 1 <= bits <= 16, num_iters >= 0,
+ * plus 0 (lin) or 1 (lin+).  No workspace.
+ */
+int po2q_quantize_lin_f32(const float* w, float* out, int64_t d0, int64_t d1, int64_t d2, int64_t d3, int bits,
+                          int num_iters, int plus, void* stream);
+
+/*
  * Quantized 2-D convolution forward (quantize weight, then conv; NCHW fp32).
  * Replaces QuantizedConv2d.forward (models/quantized_conv.py:32-38), i.e.
  * F.conv2d(x, quantize_fn.apply(weight, bits), bias, stride, padding, dilation, groups);

@@ -5,6 +5,7 @@ tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import it,
 and only as the checker / the timed CPU baseline — never as product code.
 
   quantize(w, bits, mode, fsr=1)        utils/quantizers.py:19-56
+  quantize_lin(w, bits, plus, iters)    utils/quantizers.py:59-136 (lin / lin+)
   sq_error(w, q)                        models/quantized_conv.py:40-45
   conv2d(x, w, b, stride, padding, ...) F.conv2d as called at quantized_conv.py:36,38
   qconv2d(x, w, b, ..., bits, mode)     models/quantized_conv.py:32-38
@@ -43,6 +44,8 @@ def lib():
         L.po2o_sq_error.restype = ctypes.c_double
         L.po2o_conv2d.argtypes = [p, p, p, p] + [i64] * 14
         L.po2o_conv2d.restype = None
+        L.po2o_quantize_lin.argtypes = [p, p, i64, i64, i64, i64, i32, i32, i32]
+        L.po2o_quantize_lin.restype = None
         _lib = L
     return _lib
 
@@ -64,6 +67,16 @@ def quantize(w, bits, mode, fsr=1):
     w = _f32(w)
     out = np.empty_like(w)
     lib().po2o_quantize(_ptr(w), _ptr(out), w.size, int(bits), int(fsr), MODES[mode] - 1)
+    return out
+
+
+def quantize_lin(w, bits, plus, num_iters=10):
+    """LinearPowerOfTwo(Plus)Quantizer.forward(None, w, bits, num_iters) for a 4-D fp32
+    weight (utils/quantizers.py:59-136)."""
+    w = _f32(w)
+    assert w.ndim == 4
+    out = np.empty_like(w)
+    lib().po2o_quantize_lin(_ptr(w), _ptr(out), *w.shape, int(bits), int(num_iters), int(bool(plus)))
     return out
 
 

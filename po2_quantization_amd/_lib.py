@@ -25,6 +25,7 @@ EXPORTS = (
     "po2q_last_error",
     "po2q_quantize_workspace_bytes",
     "po2q_quantize_f32",
+    "po2q_quantize_lin_f32",
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
     "po2q_qconv2d_fused_f32",
@@ -72,6 +73,8 @@ def load():
     L.po2q_quantize_workspace_bytes.argtypes = [i64]
     L.po2q_quantize_f32.restype = i32
     L.po2q_quantize_f32.argtypes = [p, p, i64, i32, i32, i32, p, sz, p]
+    L.po2q_quantize_lin_f32.restype = i32
+    L.po2q_quantize_lin_f32.argtypes = [p, p, i64, i64, i64, i64, i32, i32, i32, p]
     L.po2q_qconv2d_workspace_bytes.restype = sz
     L.po2q_qconv2d_workspace_bytes.argtypes = [i64] * 14 + [i32, i32, i32, i32]
     L.po2q_qconv2d_f32.restype = i32
@@ -128,6 +131,22 @@ def quantize(w, bits, mode, fsr=1):
         ws = _workspace(L.po2q_quantize_workspace_bytes(n), wc.device)
         _check(L.po2q_quantize_f32(wc.data_ptr(), out.data_ptr(), n, int(bits), int(fsr), mode_id,
                                    ws.data_ptr(), ws.numel(), _stream(wc.device)))
+    return out
+
+
+def quantize_lin(w, bits, plus, num_iters=10):
+    """lin / lin+ quantization of a 4-D weight, per input channel (dim 1)
+    (utils/quantizers.py:59-136)."""
+    _require_hip_f32(w, "input")
+    if w.dim() != 4:
+        # the reference reduces dims 3, 2, 0 explicitly (torch.max(..., dim=3) ...)
+        raise Po2qError("po2q: the lin quantizers need a 4-D weight (got %d dims)" % w.dim())
+    L = load()
+    wc = w.contiguous()
+    out = torch.empty_like(wc)
+    with torch.cuda.device(wc.device):
+        _check(L.po2q_quantize_lin_f32(wc.data_ptr(), out.data_ptr(), *wc.shape, int(bits), int(num_iters),
+                                       1 if plus else 0, _stream(wc.device)))
     return out
 
 

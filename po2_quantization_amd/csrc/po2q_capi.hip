@@ -79,6 +79,30 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
     return hip_status(launch_quantize_plain(w, n, partial, nb, bits, fsr, mode, out, s), "quantize launch");
 }
 
+int po2q_quantize_lin_f32(const float* w, float* out, int64_t d0, int64_t d1, int64_t d2, int64_t d3, int bits,
+                          int num_iters, int plus, void* stream) {
+    if (d0 <= 0 || d1 <= 0 || d2 <= 0 || d3 <= 0) {
+        set_error("po2q: max(): Expected reduction dim to have non-zero size (lin quantizer needs a non-empty "
+                  "4-D weight)");
+        return PO2Q_ERR_INVALID;
+    }
+    if (bits < 1 || bits > 16 || num_iters < 0 || (plus != 0 && plus != 1)) {
+        set_error("po2q: lin quantizer needs 1 <= bits <= 16, num_iters >= 0, plus in {0, 1}");
+        return PO2Q_ERR_INVALID;
+    }
+    if ((int64_t)d0 * d2 * d3 > (1LL << 30) || d1 > (1LL << 30) || d0 * d1 * d2 * d3 > (1LL << 40)) {
+        set_error("po2q: lin quantizer weight too large");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!w || !out) {
+        set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    return hip_status(launch_quantize_lin(w, out, (int)d0, (int)d1, (int)(d2 * d3), bits, num_iters, plus,
+                                          reinterpret_cast<hipStream_t>(stream)),
+                      "lin quantize launch");
+}
+
 // Workspace layout: [absmax partials][scale (bf16x3)][packed weights]
 struct WsLayout {
     size_t part_bytes, scale_off, packed_off, total;

@@ -110,4 +110,8 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
 hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
                                   const float* scale, const float* bias, float* y, hipStream_t s);
 
+// lin / lin+ quantizer (po2q_lin.hip): w, out [d0, d1, rs = d2*d3], one block per d1 channel
+hipError_t launch_quantize_lin(const float* w, float* out, int d0, int d1, int rs, int bits, int num_iters, int plus,
+                               hipStream_t s);
+
 }  // namespace po2q

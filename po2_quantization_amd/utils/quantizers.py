@@ -11,9 +11,9 @@ PO2 / PO2+ run on the hand-written HIP kernels of libpo2q (fp32 HIP tensors
 only; anything else raises — there is no CPU path).  Backward is the
 straight-through estimator of the reference (:34-36, :54-56).
 
-LinearPowerOfTwo(Plus)Quantizer (utils/quantizers.py:59-136) are NOT on the
-graded hot path ("next"): they are provided as plain torch
-ops so that quantizer_dict is complete; a native kernel replaces them later.
+LinearPowerOfTwo(Plus)Quantizer (utils/quantizers.py:59-136)
+run on the native per-channel kernel po2q_quantize_lin_f32 (po2q_lin.hip):
+fp32 HIP 4-D weights only, like the PO2 classes.
 """
 from typing import Callable, Optional
 
@@ -50,34 +50,13 @@ class PowerOfTwoPlusQuantizer(torch.autograd.Function):
 NATIVE_MODES = {PowerOfTwoQuantizer: "po2", PowerOfTwoPlusQuantizer: "po2+"}
 
 
-def quantize_per_filter(x: torch.Tensor, delta: torch.Tensor, bits: int) -> torch.Tensor:
-    """Uniform quantizer with a per-input-channel step (utils/quantizers.py:8-16)."""
-    d = delta.view(-1, 1, 1)
-    lim = (2 ** (bits - 1)) - 1
-    return d * torch.clamp(torch.round(x / d), min=-lim, max=lim)
-
-
-def _linear_po2(input: torch.Tensor, bits: int, num_iters: int, plus: bool) -> torch.Tensor:
-    # per input-channel (dim 1) range -> initial step (quantizers.py:62-69)
-    hi = input.amax(dim=(0, 2, 3))
-    lo = input.amin(dim=(0, 2, 3))
-    delta = (hi - lo) / (2 ** bits - 1)
-    q = quantize_per_filter(input, delta, bits) / delta.view(-1, 1, 1)
-    shrink = torch.sqrt(torch.tensor(8.0 / 9.0)) if plus else None
-    for _ in range(num_iters):
-        # least-squares step, then snap it to a power of two (quantizers.py:74-87 / :114-127)
-        qtw = torch.sum(q * input, dim=[0, 2, 3])
-        qtq = torch.sum(q * q, dim=[0, 2, 3])
-        delta = qtw / qtq
-        delta = 2 ** torch.round(torch.log2(shrink.to(delta.device) * delta if plus else delta))
-        q = quantize_per_filter(input, delta, bits) / delta.view(-1, 1, 1)
-    return q * delta.view(-1, 1, 1)
-
-
 class LinearPowerOfTwoQuantizer(torch.autograd.Function):
+    """Per-input-channel uniform grid with a power-of-two step refit num_iters times
+    (utils/quantizers.py:59-96)."""
+
     @staticmethod
     def forward(ctx, input: torch.Tensor, bits: int = 4, num_iters: int = 10):
-        return _linear_po2(input, bits, num_iters, plus=False)
+        return _lib.quantize_lin(input, bits, plus=False, num_iters=num_iters)
 
     @staticmethod
     def backward(ctx, grad_output):
@@ -85,9 +64,11 @@ class LinearPowerOfTwoQuantizer(torch.autograd.Function):
 
 
 class LinearPowerOfTwoPlusQuantizer(torch.autograd.Function):
+    """lin with the step snapped as 2^round(log2(sqrt(8/9) delta)) (utils/quantizers.py:99-136)."""
+
     @staticmethod
     def forward(ctx, input: torch.Tensor, bits: int = 4, num_iters: int = 10):
-        return _linear_po2(input, bits, num_iters, plus=True)
+        return _lib.quantize_lin(input, bits, plus=True, num_iters=num_iters)
 
     @staticmethod
     def backward(ctx, grad_output):

@@ -12,6 +12,8 @@ Writes (all data, no reference source):
   models.npz      ResNet20 PTQ (config 1: quantize_model, quantizers.py:139-153)
                   and QAT-mode logits for ResNet20 / ResNet56 / MobileNetV2 on
                   seeded synthetic inputs; weights come from fill.seeded_fill_
+  lin_kat.npz     LinearPowerOfTwo(Plus)Quantizer vectors (utils/quantizers.py:59-136),
+                  inputs + outputs, bits 2/3/4, default and explicit num_iters
   models.json     state_dict key/shape lists of the reference models (checkpoint
                   compatibility of the drop-in modules)
 """
@@ -152,6 +154,41 @@ def gen_conv():
     print("conv_kat.npz:", len(meta), "cases")
 
 
+LIN_SHAPES = {"r16": (16, 16, 3, 3), "r32_16": (32, 16, 3, 3), "r64": (64, 64, 3, 3), "ds1x1": (64, 32, 1, 1),
+              "pw": (144, 24, 1, 1), "dw": (96, 1, 3, 3), "fusion": (24, 48, 3, 3), "odd": (7, 5, 3, 1)}
+
+
+def gen_lin():
+    from utils.quantizers import LinearPowerOfTwoPlusQuantizer, LinearPowerOfTwoQuantizer
+
+    qs = {"lin": LinearPowerOfTwoQuantizer, "lin+": LinearPowerOfTwoPlusQuantizer}
+    g = torch.Generator().manual_seed(4321)
+    cases = {}
+    for sname, shp in LIN_SHAPES.items():
+        fan = shp[0] * shp[2] * shp[3]
+        for dec in (-2, 0):
+            cases["%s_e%d" % (sname, dec)] = (torch.randn(shp, generator=g) * (2.0 / fan) ** 0.5 * 10.0 ** dec).numpy()
+    # skewed channels (min and max of different magnitude), a constant channel
+    # (delta 0 -> NaN, as in the reference), a channel holding a NaN, an all-zero tensor
+    w = torch.randn((8, 6, 3, 3), generator=g) * 0.05
+    w[:, 1] = w[:, 1].abs() + 0.02
+    w[:, 2] = 0.125
+    w[3, 4, 1, 1] = float("nan")
+    cases["edge"] = w.numpy()
+    cases["zeros"] = np.zeros((4, 3, 3, 3), dtype=np.float32)
+    out = {}
+    for name, x in cases.items():
+        out["x/" + name] = x
+        for qn, q in qs.items():
+            for bits in (2, 3, 4):
+                out["y/%s/%s/%d" % (name, qn, bits)] = q.forward(None, torch.from_numpy(x.copy()), bits).numpy()
+            out["apply/%s/%s/4" % (name, qn)] = q.apply(torch.from_numpy(x.copy()), 4).numpy()
+            for it in (0, 3):
+                out["it%d/%s/%s/4" % (it, name, qn)] = q.forward(None, torch.from_numpy(x.copy()), 4, it).numpy()
+    np.savez_compressed(os.path.join(HERE, "lin_kat.npz"), **out)
+    print("lin_kat.npz:", len(out), "arrays")
+
+
 def gen_models():
     from models.model import get_model
     from utils.quantizers import quantize_model, quantizer_dict
@@ -201,9 +238,15 @@ def main():
     sys.path.insert(0, REF)
     thr = json.load(open(os.path.join(HERE, "po2_thresholds.json")))["modes"]
     torch.set_num_threads(8)
-    gen_quant(thr)
-    gen_conv()
-    gen_models()
+    parts = sys.argv[1:] or ["quant", "conv", "lin", "models"]  # e.g. `gen_golden.py lin`
+    if "quant" in parts:
+        gen_quant(thr)
+    if "conv" in parts:
+        gen_conv()
+    if "lin" in parts:
+        gen_lin()
+    if "models" in parts:
+        gen_models()
 
 
 if __name__ == "__main__":

@@ -8,7 +8,7 @@ from oracle import oracle as O
 from po2_quantization_amd import _lib
 from po2_quantization_amd.utils.quantizers import (PowerOfTwoPlusQuantizer, PowerOfTwoQuantizer,
                                                    quantizer_dict)
-from tests._util import bits_equal, quant_kat_items
+from tests._util import bits_equal, lin_kat_items, quant_kat_items
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -111,3 +111,51 @@ def test_stream_semantics_no_host_sync():
     torch.cuda.synchronize()
     ref = O.quantize((w * 3.0).cpu().numpy(), 4, "po2")
     assert bits_equal(out.cpu().numpy(), ref).all()
+
+
+# ---- lin / lin+ (utils/quantizers.py:59-136) ----
+
+def test_lin_every_golden_vector_bit_exact():
+    d, items = lin_kat_items()
+    for key, name, qn, bits, iters, kind in items:
+        x = torch.from_numpy(d["x/" + name].copy()).to(DEV)
+        q = quantizer_dict[qn]
+        if kind == "apply":
+            y = q.apply(x, bits)
+        elif kind.startswith("it"):
+            y = q.forward(None, x, bits, iters)
+        else:
+            y = q.forward(None, x, bits=bits)
+        ok = bits_equal(y.cpu().numpy(), d[key])
+        assert ok.all(), (key, np.nonzero(~ok.ravel())[0][:8])
+
+
+@pytest.mark.parametrize("shape", [(16, 16, 3, 3), (64, 64, 3, 3), (960, 160, 1, 1), (96, 1, 3, 3),
+                                   (5000, 2, 1, 1), (17000, 1, 1, 1), (3, 7, 5, 2), (1, 1, 1, 1)])
+@pytest.mark.parametrize("qn", ["lin", "lin+"])
+def test_lin_random_weights_match_oracle(shape, qn):
+    """Random weights over three decades, every kernel path (channels of <= 4096, <= 16384
+    and more elements): bit-exact with the oracle."""
+    g = torch.Generator().manual_seed(sum(shape))
+    for dec in (-3, -1, 1):
+        w = torch.randn(shape, generator=g) * 10.0 ** dec
+        for bits in (2, 3, 4, 8):
+            y = _lib.quantize_lin(w.to(DEV), bits, qn == "lin+").cpu().numpy()
+            ref = O.quantize_lin(w.numpy(), bits, qn == "lin+")
+            ok = bits_equal(y, ref)
+            assert ok.all(), (shape, dec, bits, np.nonzero(~ok.ravel())[0][:8])
+
+
+def test_lin_errors_and_autograd():
+    w = torch.randn(8, 4, 3, 3, device=DEV, requires_grad=True)
+    y = quantizer_dict["lin"].apply(w, 4)
+    y.sum().backward()  # straight-through (quantizers.py:93-96)
+    assert torch.equal(w.grad, torch.ones_like(w))
+    with pytest.raises(_lib.Po2qError, match="4-D"):
+        _lib.quantize_lin(torch.randn(8, 4, device=DEV), 4, False)
+    with pytest.raises(_lib.Po2qError, match="non-zero size"):
+        _lib.quantize_lin(torch.randn(0, 4, 3, 3, device=DEV), 4, False)
+    with pytest.raises(_lib.Po2qError, match="bits"):
+        _lib.quantize_lin(torch.randn(2, 4, 3, 3, device=DEV), 0, False)
+    with pytest.raises(_lib.Po2qError, match="HIP device"):
+        _lib.quantize_lin(torch.randn(2, 4, 3, 3), 4, False)

@@ -1,10 +1,12 @@
 """CPU: pin the oracle (oracle/) against the golden vectors produced by running
 the reference (tests/golden/gen_golden.py).  No GPU."""
+import os
+
 import numpy as np
 import pytest
 
 from oracle import oracle as O
-from tests._util import CONV_TOL, bits_equal, load_json, load_npz, normwise_err, quant_kat_items
+from tests._util import CONV_TOL, bits_equal, lin_kat_items, load_json, load_npz, normwise_err, quant_kat_items
 
 
 def test_quantizer_bit_exact_on_every_golden_vector():
@@ -73,3 +75,30 @@ def test_sq_error():
     w = np.random.default_rng(0).standard_normal(1000).astype(np.float32)
     q = O.quantize(w, 4, "po2+")
     assert abs(O.sq_error(w, q) - float(((q.astype(np.float64) - w) ** 2).sum())) < 1e-9
+
+
+def test_lin_oracle_bit_exact_on_every_golden_vector():
+    """lin / lin+ restatement vs the reference's outputs (utils/quantizers.py:59-136):
+    bits 2/3/4, num_iters 0/3/10, constant and NaN channels, all-zero tensor."""
+    d, items = lin_kat_items()
+    assert len(items) >= 200
+    for key, name, qn, bits, iters, _ in items:
+        y = O.quantize_lin(d["x/" + name], bits, qn == "lin+", iters)
+        ok = bits_equal(y, d[key])
+        assert ok.all(), (key, np.nonzero(~ok.ravel())[0][:8])
+
+
+def test_log2_tables_agree():
+    """The product's and the oracle's generated round(log2) tables are the same data
+    (tools/gen_log2_table.py) and reproduce the PO2 rows of SURVEY §8a."""
+    import re
+
+    def read(path):
+        txt = open(path).read()
+        return [int(v, 16) for v in re.findall(r"0x([0-9a-f]{8})u", txt)]
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    a = read(os.path.join(root, "po2_quantization_amd/csrc/po2q_log2_table.h"))
+    b = read(os.path.join(root, "oracle/po2_oracle_log2_table.h"))
+    assert a == b and len(a) == 254
+    assert a[-1 + 126] == 0x3F3504F3 and a[-5 + 126] == 0x3D3504F2  # k = -1, -5 (PO2 T_k)
