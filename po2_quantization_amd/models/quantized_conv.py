@@ -42,13 +42,12 @@ class _QConv2dFn(torch.autograd.Function):
         x, weight, bias = ctx.saved_tensors
         stride, padding, dilation, groups, bits, mode = ctx.conf
         qw = weight if mode == "none" else _lib.quantize(weight, bits, mode)
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.nn.grad.conv2d_input(x.shape, qw, gy, stride, padding, dilation, groups)
-        if ctx.needs_input_grad[1]:  # STE: d qw / d w = 1
-            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, stride, padding, dilation, groups)
-        if bias is not None and ctx.needs_input_grad[2]:
-            gb = gy.sum(dim=(0, 2, 3))
+        # one convolution_backward for the input, weight (STE: d qw / d w = 1) and bias
+        # gradients, as autograd issues for F.conv2d(x, qw, bias)
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]]
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            gy, x, qw, None if bias is None else [bias.shape[0]], list(stride), list(padding), list(dilation),
+            False, [0, 0], groups, mask)
         return gx, gw, gb, None, None, None, None, None, None, None
 
 

@@ -1,0 +1,96 @@
+"""QAT training on the drop-in modules (po2_quantization_amd/qat.py):
+gradients of the fused native forward + STE backward equal torch autograd of the
+reference formulation; the train loop runs the reference's schedule; DDP keeps ranks
+in lock-step (2 processes on one GPU, gloo).  GPU only."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from po2_quantization_amd import _lib, qat
+from po2_quantization_amd.models import quantized_conv as QC
+from po2_quantization_amd.models.model import get_model
+from po2_quantization_amd.utils.quantizers import quantizer_dict
+from tests._util import CONV_TOL
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _torch_forward(self, input):
+    """The reference's QuantizedConv2d.forward in torch ops (quantized_conv.py:32-38) with
+    the quantizer's straight-through backward (quantizers.py:34-36)."""
+    if self.quantize_fn is None:
+        return F.conv2d(input, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+    qw = self.quantize_fn.apply(self.weight, self.bits)
+    w = self.weight + (qw - self.weight).detach()
+    return F.conv2d(input, w, self.bias, self.stride, self.padding, self.dilation, self.groups)
+
+
+@pytest.mark.parametrize("qn", ["po2", "po2+", "lin"])
+def test_qat_gradients_match_torch_autograd(qn, monkeypatch):
+    torch.manual_seed(0)
+    m = get_model("resnet20", 10, quantizer_dict[qn], 4, (32, 32)).to(DEV).train()
+    x = torch.randn(16, 3, 32, 32, device=DEV)
+    y = torch.randint(0, 10, (16,), device=DEV)
+    F.cross_entropy(m(x), y).backward()
+    g_native = {k: p.grad.clone() for k, p in m.named_parameters()}
+    m.zero_grad()
+    monkeypatch.setattr(QC.QuantizedConv2d, "forward", _torch_forward)
+    F.cross_entropy(m(x), y).backward()
+    for k, p in m.named_parameters():
+        a, b = g_native[k], p.grad
+        err = ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+        assert err <= 100 * CONV_TOL, (k, err)  # gradients pass ~20 layers of backward
+
+
+def test_train_loop_reference_schedule(tmp_path):
+    torch.manual_seed(1)
+    m = qat.build_model("resnet20", 10, quantizer_dict["po2"], 4, (32, 32), torch.device(DEV))
+    images = torch.randn(96, 3, 32, 32)
+    labels = (images.mean(dim=(1, 2, 3)) > 0).long()  # a learnable synthetic task
+    rows = qat.run_train_loop(m, torch.device(DEV), images, labels, 32, str(tmp_path / "po2_4.pth"),
+                              num_epochs=4, lr=0.02, log=lambda s: None)
+    assert [r[0] for r in rows] == [0, 1, 2, 3]
+    assert all(torch.isfinite(torch.tensor(r[1])) and 0.0 <= r[2] <= 1.0 and r[3] > 0 for r in rows)
+    assert rows[-1][1] < rows[0][1]  # loss goes down
+    qat.write_train_csv(str(tmp_path / "po2_4.csv"), rows)
+    assert open(tmp_path / "po2_4.csv").readline().strip() == "epoch,train_loss,train_acc,quantization_error"
+    sd = torch.load(tmp_path / "po2_4.pth", weights_only=True)
+    assert set(sd) == set(m.state_dict())
+
+
+def _ddp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
+    m = qat.build_model("resnet20", 10, quantizer_dict["po2+"], 4, (32, 32), torch.device(DEV), sync_bn=False)
+    opt, _, _, _ = qat.make_optimizer(m, 0.01, 10)
+    crit = torch.nn.CrossEntropyLoss()
+    g = torch.Generator().manual_seed(5)
+    images = torch.randn(32, 3, 32, 32, generator=g)
+    labels = torch.randint(0, 10, (32,), generator=g)
+    for x, y in qat.shard_batches(images, labels, 8, epoch=0):
+        qat.train_step(m, opt, crit, x.to(DEV), y.to(DEV))
+    flat = torch.cat([p.detach().flatten() for p in m.parameters()]).cpu()
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    torch.distributed.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save(torch.stack(gathered), out)
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_two_ranks_stay_in_lockstep(tmp_path):
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "params.pt")
+    mp.spawn(_ddp_worker, args=(2, port, out), nprocs=2, join=True)
+    p = torch.load(out, weights_only=True)
+    assert torch.equal(p[0], p[1])  # averaged gradients -> identical updates
+    assert _lib.load() is not None

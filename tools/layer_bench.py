@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--precision", default="auto")
     ap.add_argument("--mode", default="po2")
     ap.add_argument("--torch", action="store_true", help="also time torch F.conv2d (MIOpen) on the same shapes")
+    ap.add_argument("--tune", action="store_true", help="autotune each shape first (cudnn.benchmark counterpart)")
     args = ap.parse_args()
+    if args.tune:
+        _lib.benchmark = True
     nb = {"resnet20": 3, "resnet32": 5, "resnet44": 7, "resnet56": 9}[args.model]
     dev = torch.device("cuda:0")
     seen, shapes, H = {}, [], args.image
