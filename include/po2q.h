@@ -163,6 +163,32 @@ int po2q_qconv2d_f32_plan(int index, const float* x, const float* w, const float
                           void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * po2q_qconv2d_f32 in two enqueues, so the weight quantize + pack can run on another
+ * stream, ahead of (and overlapped with) earlier convolutions:
+ *   po2q_qconv2d_pack_f32    quantizes w and packs it into `workspace` (x, y untouched)
+ *   po2q_qconv2d_packed_f32  runs the conv from that workspace (w untouched)
+ * Same arguments and workspace size as po2q_qconv2d_f32; `plan` is -1 for the plan
+ * po2q_qconv2d_f32 would run (tuned or heuristic) or a candidate index (as
+ * po2q_qconv2d_f32_plan) -- both calls must name the same plan.  Ordering between the
+ * two (and against later writes of w / reuse of the workspace) is the caller's, e.g. HIP
+ * events; on one stream the pair equals po2q_qconv2d_f32 bit for bit.
+ */
+int po2q_qconv2d_pack_f32(int plan, const float* w,
+                          int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t K, int64_t R, int64_t S,
+                          int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                          int64_t dil_h, int64_t dil_w, int64_t groups,
+                          int bits, int fsr, int mode, int flags,
+                          void* workspace, size_t workspace_bytes, void* stream);
+int po2q_qconv2d_packed_f32(int plan, const float* x, const float* bias, float* y,
+                            int64_t N, int64_t C, int64_t H, int64_t W,
+                            int64_t K, int64_t R, int64_t S,
+                            int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                            int64_t dil_h, int64_t dil_w, int64_t groups,
+                            int bits, int fsr, int mode, int flags,
+                            const void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * Diagnostic: the plan po2q_qconv2d_f32 would run for these arguments, as a
  * NUL-terminated text ("kind=bf16x3 CC=16 NT=1 NJ=4 tile=8x32 ..."), written
  * to buf (truncated to len).  No reference counterpart; used by bench.py and

@@ -29,6 +29,8 @@ EXPORTS = (
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
     "po2q_qconv2d_fused_f32",
+    "po2q_qconv2d_pack_f32",
+    "po2q_qconv2d_packed_f32",
     "po2q_qconv2d_autotune",
     "po2q_qconv2d_plans",
     "po2q_qconv2d_f32_plan",
@@ -81,6 +83,10 @@ def load():
     L.po2q_qconv2d_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
     L.po2q_qconv2d_fused_f32.restype = i32
     L.po2q_qconv2d_fused_f32.argtypes = [p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, p, p, i32, p, sz, p]
+    L.po2q_qconv2d_pack_f32.restype = i32
+    L.po2q_qconv2d_pack_f32.argtypes = [i32, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
+    L.po2q_qconv2d_packed_f32.restype = i32
+    L.po2q_qconv2d_packed_f32.argtypes = [i32, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
     L.po2q_qconv2d_autotune.restype = i32
     L.po2q_qconv2d_autotune.argtypes = ([p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
                                         + [ctypes.c_char_p, sz])
@@ -255,6 +261,56 @@ def qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bi
                                         ptr(ext[0]), ptr(ext[1]), ptr(rc), ACTS[act],
                                         ws.data_ptr(), ws.numel(), _stream(xc.device)))
     return y
+
+
+class SplitConv:
+    """One quantized conv layer as two enqueues (po2q_qconv2d_pack_f32 /
+    po2q_qconv2d_packed_f32): the weight quantize + pack into a workspace this object
+    owns, then the conv from it.  pack() may run on another stream than conv(); the
+    caller orders them (events) and must not re-pack while a conv still reads the
+    workspace.  The plan is the one qconv2d() runs for these arguments (call qconv2d
+    once first when autotuning)."""
+
+    def __init__(self, x_shape, w, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+                 precision="auto"):
+        _require_hip_f32(w, "weight")
+        N, C, H, W = (int(v) for v in x_shape)
+        K, Cg, R, S = w.shape
+        sh, sw = _pair(stride)
+        ph, pw = _pair(padding)
+        dh, dw = _pair(dilation)
+        self.w = w.contiguous()
+        self.key = (N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, int(groups), int(bits), int(fsr), MODES[mode],
+                    PRECISIONS[precision])
+        P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+        Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+        self.yshape = (N, K, P, Q)
+        L = load()
+        nbytes = L.po2q_qconv2d_workspace_bytes(*self.key)
+        if nbytes == 0:
+            _check(1)
+        self.ws = _workspace(nbytes, w.device)
+
+    def _plan(self):
+        idx = _saved_plan(self.key)
+        return -1 if idx is None else int(idx)
+
+    def pack(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.w.device)
+        _check(load().po2q_qconv2d_pack_f32(self._plan(), self.w.data_ptr(), *self.key, self.ws.data_ptr(),
+                                            self.ws.numel(), ctypes.c_void_p(s.cuda_stream)))
+
+    def conv(self, x, bias=None):
+        _require_hip_f32(x, "input")
+        if tuple(x.shape) != tuple(self.key[:4]):
+            raise Po2qError("po2q: input shape %s does not match the packed layer's %s"
+                            % (list(x.shape), list(self.key[:4])))
+        xc = x.contiguous()
+        y = torch.empty(self.yshape, dtype=torch.float32, device=xc.device)
+        bp = bias.contiguous().data_ptr() if bias is not None else None
+        _check(load().po2q_qconv2d_packed_f32(self._plan(), xc.data_ptr(), bp, y.data_ptr(), *self.key,
+                                              self.ws.data_ptr(), self.ws.numel(), _stream(xc.device)))
+        return y
 
 
 def _tune_key(key):

@@ -155,11 +155,14 @@ static int check_conv_args(const float* x, const float* w, float* y, void* works
     return PO2Q_OK;
 }
 
+// phases of run_plan: the weight quantize + pack into the workspace, the conv from it
+enum { RUN_PACK = 1, RUN_CONV = 2, RUN_ALL = 3 };
+
 // Enqueue the fused quantize(+pack) and conv of plan p on stream s (+ the epilogue e:
 // in the row kernels' store epilogue where they support it, else one elementwise pass).
 static int run_plan(const ConvPlan& p, const float* x, const float* w, const float* bias, float* y, int bits, int fsr,
                     int mode, void* workspace, size_t workspace_bytes, hipStream_t s,
-                    const ConvEpi& e = ConvEpi{nullptr, nullptr, nullptr, 0}) {
+                    const ConvEpi& e = ConvEpi{nullptr, nullptr, nullptr, 0}, int phases = RUN_ALL) {
     const WsLayout L = ws_layout(p, mode);
     if (workspace_bytes < L.total) {
         set_error("po2q: conv workspace too small (need " + std::to_string(L.total) + " bytes)");
@@ -171,15 +174,18 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     void* packed = ws + L.packed_off;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
     int st;
-    if (L.nparts > 0) {
+    if ((phases & RUN_PACK) && L.nparts > 0) {
         st = hip_status(launch_absmax(w, nw, partial, L.nparts, s), "absmax launch");
         if (st) return st;
     }
     if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) {
-        st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
-                                           reinterpret_cast<uint16_t*>(packed), scale, s),
-                        "weight pack launch");
-        if (st) return st;
+        if (phases & RUN_PACK) {
+            st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
+                                               reinterpret_cast<uint16_t*>(packed), scale, s),
+                            "weight pack launch");
+            if (st) return st;
+        }
+        if (!(phases & RUN_CONV)) return PO2Q_OK;
         const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
         hipError_t he;
         bool fused_affine = false;
@@ -198,9 +204,13 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         if (st || !e.any() || (fused_affine && !e.res)) return st;
         return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, fused_affine, s), "epilogue launch");
     }
-    st = hip_status(launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
-                    "weight pack launch");
-    if (st) return st;
+    if (phases & RUN_PACK) {
+        st = hip_status(
+            launch_pack_weights(p, w, partial, L.nparts, bits, fsr, mode, reinterpret_cast<float*>(packed), s),
+            "weight pack launch");
+        if (st) return st;
+    }
+    if (!(phases & RUN_CONV)) return PO2Q_OK;
     st = hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
     if (st || !e.any()) return st;
     return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, false, s), "epilogue launch");
@@ -340,6 +350,57 @@ int po2q_qconv2d_f32_plan(int index, const float* x, const float* w, const float
     }
     return run_plan(cands[index], x, w, bias, y, bits, fsr, mode, workspace, workspace_bytes,
                     reinterpret_cast<hipStream_t>(stream));
+}
+
+// Plan `index` (>= 0: a candidate of plan_candidates, -1: the tuned / heuristic plan).
+static int pick_plan(ConvPlan& p, int index, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                     int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                     int64_t groups, int mode, int bits, int fsr, int flags) {
+    if (index < 0) {
+        if (!make_plan(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags))
+            return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+        return PO2Q_OK;
+    }
+    std::vector<ConvPlan> cands;
+    if (!plan_candidates(cands, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags))
+        return flags == PO2Q_PREC_BF16X3 ? PO2Q_ERR_UNSUPPORTED : PO2Q_ERR_INVALID;
+    if (index >= (int)cands.size()) {
+        set_error("po2q: plan index " + std::to_string(index) + " out of range [0, " + std::to_string(cands.size()) +
+                  ")");
+        return PO2Q_ERR_INVALID;
+    }
+    p = cands[index];
+    return PO2Q_OK;
+}
+
+int po2q_qconv2d_pack_f32(int plan, const float* w, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
+                          int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                          int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+    // the conv-argument checks of po2q_qconv2d_f32 (x and y are not touched here)
+    int st = check_conv_args(w, w, const_cast<float*>(w), workspace, mode, bits, flags);
+    if (st) return st;
+    ConvPlan p;
+    st = pick_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits,
+                   fsr, flags);
+    if (st) return st;
+    return run_plan(p, nullptr, w, nullptr, nullptr, bits, fsr, mode, workspace, workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream), ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_PACK);
+}
+
+int po2q_qconv2d_packed_f32(int plan, const float* x, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
+                            int64_t W, int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w,
+                            int64_t pad_h, int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, int bits,
+                            int fsr, int mode, int flags, const void* workspace, size_t workspace_bytes,
+                            void* stream) {
+    int st = check_conv_args(x, x, y, const_cast<void*>(workspace), mode, bits, flags);
+    if (st) return st;
+    ConvPlan p;
+    st = pick_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits,
+                   fsr, flags);
+    if (st) return st;
+    return run_plan(p, x, nullptr, bias, y, bits, fsr, mode, const_cast<void*>(workspace), workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream), ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_CONV);
 }
 
 int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,

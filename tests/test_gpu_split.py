@@ -1,0 +1,38 @@
+"""GPU: the two-enqueue form of the fused op (po2q_qconv2d_pack_f32 +
+po2q_qconv2d_packed_f32, _lib.SplitConv) equals po2q_qconv2d_f32 bit for bit, on one
+stream and with the pack on a side stream ordered by events."""
+import pytest
+import torch
+
+from po2_quantization_amd import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+SHAPES = [(2, 16, 20, 24, 16, 3, 1, 1), (2, 32, 16, 16, 32, 3, 1, 1), (1, 64, 9, 12, 64, 3, 1, 1),
+          (2, 16, 18, 18, 32, 3, 2, 1), (2, 32, 10, 10, 64, 1, 2, 0), (2, 8, 7, 7, 12, 5, 1, 2)]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+", "none"])
+def test_split_equals_fused_call(shape, mode):
+    N, C, H, W, K, R, st, pad = shape
+    torch.manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, device=DEV)
+    w = torch.randn(K, C, R, R, device=DEV) * 0.1
+    b = torch.randn(K, device=DEV)
+    ref = _lib.qconv2d(x, w, b, st, pad, 1, 1, 4, mode)
+    sc = _lib.SplitConv(x.shape, w, st, pad, 1, 1, 4, mode)
+    sc.pack()
+    assert torch.equal(sc.conv(x, b), ref)
+    side = torch.cuda.Stream(DEV)
+    ev = torch.cuda.Event()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        sc2 = _lib.SplitConv(x.shape, w, st, pad, 1, 1, 4, mode)
+        sc2.pack(side)
+        ev.record(side)
+    torch.cuda.current_stream().wait_event(ev)
+    assert torch.equal(sc2.conv(x, b), ref)
+    with pytest.raises(_lib.Po2qError, match="does not match"):
+        sc.conv(torch.randn(N, C, H + 1, W, device=DEV))
