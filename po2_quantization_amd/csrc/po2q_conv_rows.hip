@@ -64,8 +64,9 @@ constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x S
 constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
 
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): timing ablation bits -- 1 no MFMA,
-// 2 no split (raw bits to the planes), 4 no x loads, 8 no stores.  Product: DBG = 0.
-template <int CC, int NT, int DBG = 0, bool EPI = false>
+// 2 no split (raw bits to the planes), 4 no x loads, 8 no stores, 16 nt stores.  Product:
+// DBG = 0.  NTS: output stores with the non-temporal policy (an autotune candidate).
+template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false>
 __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const float* __restrict__ x,
                                                                      const uint4* __restrict__ wpk,
                                                                      const float* __restrict__ scale_p,
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                     const floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
                     const int q = q0 + 4 * b;
                     const uint32_t yo = (uint32_t)(nt * 16 + c) * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + q;
-                    rows_store<(DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
+                    rows_store<NTS || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
                 }
             }
             if (lane == 0) *reinterpret_cast<uint4*>(slab + zero_off) = make_uint4(0u, 0u, 0u, 0u);
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                     v[1] = outv(acc[D][grp][nt][1], nt);
                     v[2] = outv(acc[D][grp][nt][2], nt);
                     v[3] = outv(acc[D][grp][nt][3], nt);
-                    rows_store<(DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    rows_store<NTS || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
             }
         }
@@ -336,11 +337,11 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
         load_row(0, 0);
         if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store<(DBG & 16) != 0>(ry, 0x7fffffffu, z);
+            for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
         load_row(1, 1);
         if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store<(DBG & 16) != 0>(ry, 0x7fffffffu, z);
+            for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
     }
     // steps past nrows DMA zeros (out of range) and store nothing: at most 5 per item
     for (int j = 0; j < nrows; j += 6) {
@@ -419,9 +420,20 @@ void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vec
         // cost comparable with the other bf16x3 planners (their cost ~ 1.0 + overheads)
         out.push_back({0.9 + 0.001 * i, c});
     }
+    // the same with non-temporal output stores (interleaved A/B on stage 1: 4-5 % faster
+    // on some boxes, r01_v14; the autotuner decides)
+    for (int i = 0; i < (int)rbs.size() && i < 3; ++i) {
+        ConvPlan c = p;
+        c.TP = rbs[i].second;
+        c.tilesP = cdivr(p.P, c.TP);
+        const int64_t items = (int64_t)p.N * c.tilesP * c.tilesQ;
+        c.blocks = ((items + 3) / 4 + 7) / 8 * 8;
+        c.nts = 1;
+        out.push_back({0.905 + 0.001 * i, c});
+    }
 }
 
-template <int CC, int NT, int DBG = 0, bool EPI = false>
+template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false>
 static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, hipStream_t s, const float* ps = nullptr,
                                 const float* pb = nullptr, int act = 0) {
@@ -436,7 +448,7 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
     a.ps = ps;
     a.pb = pb;
     a.act = act;
-    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
@@ -469,6 +481,12 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
     }
 #endif
     // the planner only emits the variants that fit their register budget without spilling
+    if (p.nts) {
+        if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1, 0, false, true>(p, x, packed, scale, bias, y, s);
+        if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, false, true>(p, x, packed, scale, bias, y, s);
+        if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, false, true>(p, x, packed, scale, bias, y, s);
+        return hipErrorInvalidValue;
+    }
     if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1>(p, x, packed, scale, bias, y, s);
     if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1>(p, x, packed, scale, bias, y, s);
     if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2>(p, x, packed, scale, bias, y, s);
@@ -483,6 +501,15 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s) {
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true);
+    if (p.nts) {
+        if (p.CC == 16 && p.NT == 1)
+            return launch_rows_t<16, 1, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
+        if (p.CC == 32 && p.NT == 1)
+            return launch_rows_t<32, 1, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
+        if (p.CC == 32 && p.NT == 2)
+            return launch_rows_t<32, 2, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
+        return hipErrorInvalidValue;
+    }
     if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
     if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
     if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);

@@ -47,6 +47,7 @@ struct ConvPlan {
     int taps;                    // R*S
     int vrx;                     // bf16x3: row-reuse schedule, waves across (0 = generic k-step schedule)
     int pd;                      // bf16x3 register kernel: x prefetch distance in work items (1 or 2)
+    int nts;                     // row kernel (vrx 0): non-temporal output stores
     int dma_d0, dma_nck, dma_ni, dma_nw;  // bf16x3 DMA: window offset, 16-B chunks per halo row, DMAs per wave
     int dma_waves;                // bf16x3 DMA: waves per block (4 or 8)
     int dma_ov;                   // bf16x3 DMA: overlapped pipeline (split of item i+1 under the MFMAs of item i)
