@@ -300,7 +300,7 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
     return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
 }
 
-constexpr int kTuneRegCands = 6, kTuneDmaCands = 12, kTuneRowsCands = 12;
+constexpr int kTuneRegCands = 6, kTuneDmaCands = 12, kTuneRowsCands = 16;
 
 bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                      int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,

@@ -135,7 +135,8 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 // 32 = TT stores non-temporal, 64 = no wait for the DMAs (vmcnt 31), 128 = no DMA
 // instructions in the loop, 256 = no TT tile LDS traffic.
 // Product builds: DBG = 0.
-template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0>
+// NTS: output stores with the non-temporal policy (autotune candidates, plan field nts)
+template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, bool NTS = false>
 __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
             if constexpr (!(DBG & 256)) v = *reinterpret_cast<const floatx4*>(tr + c * (kKSW * 4) + ((sb ^ (c & 7)) << 4));
             const uint32_t vo = (uint32_t)c * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + (uint32_t)q;
-            rows_store<(DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
+            rows_store<NTS || (DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
         }
     };
 
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             v[1] = outv(acc[D][grp][1]);
             v[2] = outv(acc[D][grp][2]);
             v[3] = outv(acc[D][grp][3]);
-            rows_store(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+            rows_store<NTS>(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
             acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
     };
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         auto pre = [&](auto R_) __attribute__((always_inline)) {
             load_row(R_, decltype(R_)::value);
 #pragma unroll
-            for (int i = 0; i < NGW; ++i) rows_store(ry, 0x7fffffffu, z);
+            for (int i = 0; i < NGW; ++i) rows_store<NTS>(ry, 0x7fffffffu, z);
         };
         if constexpr (LW) {
             __builtin_amdgcn_s_barrier();  // the loader has rows 0 .. PD-1 in flight, row 0 landed
@@ -487,6 +488,12 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 const int64_t items = (int64_t)p.N * d.tilesP * d.tilesQ;
                 d.blocks = (items + 7) / 8 * 8;
                 out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0) + (vrx == vrxs[0] ? 0.0 : 0.02), d});
+                // the default variants (C = 64 direct stores, C = 32 loader wave) also with
+                // non-temporal output stores
+                if ((b.C == 64 && vrx == 1) || (b.C == 32 && vrx == 3)) {
+                    d.nts = 1;
+                    out.push_back({0.905 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), d});
+                }
             }
         }
 }
@@ -503,9 +510,16 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     a.pb = pb;
     a.act = act;
 #define PO2Q_RK1(c, d, e, v, tt, lw)                                                                      \
-    if (p.C == c && p.pd == d && epi == e && p.vrx == v) {                                                   \
+    if (p.C == c && p.pd == d && epi == e && p.vrx == v && !p.nts) {                                         \
         hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e>), dim3((unsigned)p.blocks), dim3(kThreads + (lw ? 64 : 0)), \
                            p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);     \
+        return hipGetLastError();                                                                            \
+    }
+#define PO2Q_RKN(c, d, e, v, tt, lw)                                                                      \
+    if (p.C == c && p.pd == d && epi == e && p.vrx == v && p.nts) {                                          \
+        hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e, 0, true>), dim3((unsigned)p.blocks),                \
+                           dim3(kThreads + (lw ? 64 : 0)), p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), \
+                           scale, bias, y, a);                                                               \
         return hipGetLastError();                                                                            \
     }
 #define PO2Q_RK(c, d, e) PO2Q_RK1(c, d, e, 1, false, false) PO2Q_RK1(c, d, e, 2, true, false)
@@ -527,9 +541,13 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     PO2Q_RK(64, 3, false) PO2Q_RK(64, 2, false) PO2Q_RK(32, 3, false) PO2Q_RK(32, 2, false)
     PO2Q_RK(64, 3, true) PO2Q_RK(64, 2, true) PO2Q_RK(32, 3, true) PO2Q_RK(32, 2, true)
     PO2Q_RK1(32, 3, false, 3, true, true) PO2Q_RK1(32, 3, true, 3, true, true)
+    PO2Q_RKN(64, 3, false, 1, false, false) PO2Q_RKN(64, 2, false, 1, false, false)
+    PO2Q_RKN(64, 3, true, 1, false, false) PO2Q_RKN(64, 2, true, 1, false, false)
+    PO2Q_RKN(32, 3, false, 3, true, true) PO2Q_RKN(32, 3, true, 3, true, true)
 
 #undef PO2Q_RK
 #undef PO2Q_RK1
+#undef PO2Q_RKN
     return hipErrorInvalidValue;
 }
 
