@@ -196,6 +196,8 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
     L = load()
     mode_id = MODES[mode]
     prec = PRECISIONS[precision]
+    if yshape[0] == 0:  # an empty batch: torch's F.conv2d returns an empty output
+        return torch.empty(yshape, dtype=torch.float32, device=xc.device)
     with torch.cuda.device(xc.device):
         nbytes = L.po2q_qconv2d_workspace_bytes(*args, int(bits), int(fsr), mode_id, prec)
         if nbytes == 0:
@@ -247,6 +249,8 @@ def qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bi
             raise Po2qError("po2q: residual shape %s does not match the output %s"
                             % (list(residual.shape), list(yshape)))
         rc = residual.contiguous()
+    if yshape[0] == 0:
+        return torch.empty(yshape, dtype=torch.float32, device=xc.device)
     with torch.cuda.device(xc.device):
         key = args + (int(bits), int(fsr), mode_id, prec)
         nbytes = L.po2q_qconv2d_workspace_bytes(*key)

@@ -302,3 +302,12 @@ def test_fused_every_row_plan_and_rejects_bad_act():
         _lib._check(L.po2q_qconv2d_fused_f32(x.data_ptr(), w.data_ptr(), None, y.data_ptr(), N, C, H, W, K, 3, 3,
                                              1, 1, 1, 1, 1, 1, 1, 4, 1, 1, 0, None, None, None, 9,
                                              x.data_ptr(), 1 << 20, None))
+
+
+def test_empty_batch_like_torch():
+    """F.conv2d on an empty batch returns an empty [0, K, P, Q] output (quantized_conv.py:36)."""
+    w = torch.randn(8, 4, 3, 3, device=DEV)
+    y = _lib.qconv2d(torch.empty(0, 4, 9, 9, device=DEV), w, None, 2, 1)
+    assert y.shape == (0, 8, 5, 5)
+    y = _lib.qconv2d_fused(torch.empty(0, 4, 9, 9, device=DEV), w, None, 1, 1, act="relu")
+    assert y.shape == (0, 8, 9, 9)
