@@ -292,10 +292,23 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
     return plan_fallback(p);
 }
 
+bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                     int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                     int64_t groups, int mode, int bits, int fsr, int flags);
+
 bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
                int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t groups, int mode,
                int bits, int fsr, int flags) {
     if (!plan_geometry(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups)) return false;
+    if (const char* force = getenv("PO2Q_PLAN")) {  // test / tuning knob: candidate index for every call
+        std::vector<ConvPlan> cands;
+        const int idx = atoi(force);
+        if (plan_candidates(cands, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags) &&
+            idx >= 0 && idx < (int)cands.size()) {
+            p = cands[idx];
+            return true;
+        }
+    }
     if (!tuning_knobs() && tuned_lookup(p, mode, bits, fsr, flags)) return true;
     return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
 }

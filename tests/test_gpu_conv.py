@@ -311,3 +311,28 @@ def test_empty_batch_like_torch():
     assert y.shape == (0, 8, 5, 5)
     y = _lib.qconv2d_fused(torch.empty(0, 4, 9, 9, device=DEV), w, None, 1, 1, act="relu")
     assert y.shape == (0, 8, 9, 9)
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 20, 32, 16), (1, 32, 13, 36, 32), (1, 64, 9, 40, 64)],
+                         ids=["c16", "c32", "c64"])
+def test_fused_epilogue_every_candidate_plan(shape, monkeypatch):
+    """The fused entry (affine + activation in the row kernels' store epilogue, residual as
+    a pass) through every candidate plan (PO2Q_PLAN forces candidate i): tile, TT, loader
+    wave and non-temporal-store variants alike."""
+    N, C, H, W, K = shape
+    torch.manual_seed(7)
+    x = torch.randn(N, C, H, W, device=DEV)
+    w = torch.randn(K, C, 3, 3, device=DEV) * 0.1
+    ps = torch.rand(K, device=DEV) + 0.5
+    pb = torch.randn(K, device=DEV) * 0.1
+    res = torch.randn(N, K, H, W, device=DEV)
+    base = _lib.qconv2d(x, w, None, 1, 1) * ps.view(1, -1, 1, 1) + pb.view(1, -1, 1, 1)
+    n = len(_lib.plans(N, C, H, W, K, 3, 3, 1, 1))
+    for i in range(n):
+        monkeypatch.setenv("PO2Q_PLAN", str(i))
+        for act, r in (("relu6", None), ("silu", res)):
+            ref = base + (r if r is not None else 0)
+            ref = torch.clamp(ref, 0, 6) if act == "relu6" else torch.nn.functional.silu(ref)
+            y = _lib.qconv2d_fused(x, w, None, 1, 1, post_scale=ps, post_shift=pb, residual=r, act=act)
+            err = ((y - ref).abs().max() / ref.abs().max()).item()
+            assert err <= CONV_TOL, (i, act, err)
