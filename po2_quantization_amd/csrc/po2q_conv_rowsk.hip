@@ -68,6 +68,7 @@ struct RowsKArgs {
     const float* ps;  // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
     const float* pb;
     int act;
+    const float* res;  // RES: y = act(y * ps + pb + res), res [N, K, P, Q] (loader wave DMAs it)
 };
 
 // The LW loader wave: every DMA of the block, the layout the MFMA waves' own DMAs
@@ -77,9 +78,9 @@ struct RowsKArgs {
 // its slot is refilled with row j + PD after the barrier of step j, so it executes
 // exactly the MFMA waves' barriers: one preamble, one per (whole-triple) step and the
 // TT flush.
-template <int C, int PD, bool TT>
+template <int C, int PD, bool TT, bool RES>
 __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const RowsKArgs& a, unsigned char* raw,
-                                            int n, int q0, int p0, int nrows) {
+                                            unsigned char* resb, int n, int q0, int p0, int nrows, int rbe) {
     constexpr int NI = C / 8 + 1;  // instructions per row: C/8 interior + 1 halo
     static_assert(2 * C <= 64, "one halo instruction per row");
     const int lane = threadIdx.x & 63;
@@ -94,6 +95,19 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
     const bool qh_ok = gqh >= 0 && gqh < a.W;
     const uint32_t vh0 = (uint32_t)hch * cstride + (uint32_t)gqh * 4u;
     const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    // RES: the residual row stored in step js (output row p0 + js - 3) into slot js & 1,
+    // [K][32 columns] like the output tile (unswizzled): 8 channels x 128 B per instruction
+    const int PQ = a.P * a.Q;
+    const __amdgpu_buffer_rsrc_t rr = rows_rsrc(RES ? a.res + (int64_t)n * C * PQ : x, RES ? C * PQ * 4 : 4);
+    const uint32_t vr0 = (uint32_t)(lane >> 3) * (uint32_t)PQ * 4u + (uint32_t)gq4 * 4u;
+    auto lres = [&](int js) __attribute__((always_inline)) {
+        const int orow = js - 3;
+        const bool ok = orow >= 0 && orow < rbe && gq4 < a.Q;
+        const uint32_t vo = ok ? vr0 + (uint32_t)(p0 + orow) * (uint32_t)a.Q * 4u : 0x7fffffffu;
+        const uint32_t base = (uint32_t)(uintptr_t)resb + (uint32_t)((js & 1) * kKTile<C>);
+#pragma unroll
+        for (int i = 0; i < C / 8; ++i) rows_dma16(rr, vo, i * 8u * (uint32_t)PQ * 4u, base + (uint32_t)i * 1024u);
+    };
     auto lrow = [&](int sl, int j) __attribute__((always_inline)) {
         const int h = p0 - 1 + j;
         const bool hok = j < nrows && h >= 0 && h < a.H;
@@ -113,10 +127,14 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
     for (int j = 0; j < steps; ++j) {
         rows_wait<(PD - 2) * NI>();  // row j + 1 (issued after it: rows j + 2 .. j + PD - 1)
         __builtin_amdgcn_s_barrier();
+        if constexpr (RES) lres(j + 1);  // older than the row DMA below: the next wait covers it
         lrow(sl, j + PD);  // the slot of row j, split before this barrier
         sl = sl + 1 == PD ? 0 : sl + 1;
     }
-    if (TT && nrows % 3 == 0) __builtin_amdgcn_s_barrier();
+    if (TT && nrows % 3 == 0) {
+        if constexpr (RES) rows_wait<0>();  // the flushed row's residual
+        __builtin_amdgcn_s_barrier();
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -136,7 +154,9 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 // instructions in the loop, 256 = no TT tile LDS traffic.
 // Product builds: DBG = 0.
 // NTS: output stores with the non-temporal policy (autotune candidates, plan field nts)
-template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, bool NTS = false>
+// RES (with LW, TT, EPI): the residual add inside the kernel (the loader wave DMAs the
+//     residual rows next to the output tile; act after the add)
+template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, bool NTS = false, bool RES = false>
 __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -159,6 +179,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
     unsigned char* planes = lds;                 // 2 buffers x 3 planes
     unsigned char* raw = lds + 2 * 3 * PL;       // PD slots
     unsigned char* tile = raw + PD * kKRawSlot<C>;  // TT: 2 output row tiles
+    unsigned char* resb = tile + 2 * kKTile<C>;     // RES: 2 residual row tiles
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -175,7 +196,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
 
     if constexpr (LW) {
         if (wave == 4) {
-            loader_wave<C, PD, TT>(x, a, raw, n, q0, p0, nrows);
+            loader_wave<C, PD, TT, RES>(x, a, raw, resb, n, q0, p0, nrows, rbe);
             return;
         }
     }
@@ -199,7 +220,9 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk), "+v"(eps_), "+v"(epb_));
     auto outv = [&](float accv) __attribute__((always_inline)) {
         const float v = accv * scale + bk;
-        if constexpr (EPI)
+        if constexpr (EPI && RES)
+            return v * eps_ + epb_;  // the activation follows the residual add (store_tile)
+        else if constexpr (EPI)
             return epi_act(v * eps_ + epb_, a.act);
         else
             return v;
@@ -265,7 +288,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
 
     // TT stores: wave w, instruction i: lane l -> channel (K/4)w + 8i + (l >> 3), columns
     // q0 + 4(l & 7) .. +3 (the tile's 16-byte blocks are XOR-swizzled by channel)
-    auto store_tile = [&](const unsigned char* tr, int o, bool orow) __attribute__((always_inline)) {
+    auto store_tile = [&](const unsigned char* tr, int o, bool orow, int rslot) __attribute__((always_inline)) {
         const int sb = lane & 7;
         const int q = q0 + 4 * sb;
 #pragma unroll
@@ -273,6 +296,11 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             const int c = (K / 4) * wave + 8 * i + (lane >> 3);
             floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
             if constexpr (!(DBG & 256)) v = *reinterpret_cast<const floatx4*>(tr + c * (kKSW * 4) + ((sb ^ (c & 7)) << 4));
+            if constexpr (RES) {
+                const floatx4 r = *reinterpret_cast<const floatx4*>(resb + rslot * kKTile<C> + c * (kKSW * 4) + 16 * sb);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e] + r[e], a.act);
+            }
             const uint32_t vo = (uint32_t)c * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + (uint32_t)q;
             rows_store<NTS || (DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
         }
@@ -351,7 +379,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             // store the row completed in the previous step (tile 1 - B2, published by
             // this step's barrier), then park this step's row in tile B2
             // (the loop runs whole triples of steps: steps past nrows - 1 only store)
-            store_tile(tile + (1 - B2) * kKTile<C>, p0 + j - 3, j >= 3 && j - 3 < rbe);
+            store_tile(tile + (1 - B2) * kKTile<C>, p0 + j - 3, j >= 3 && j - 3 < rbe, B2);
             unsigned char* tw = tile + B2 * kKTile<C>;
 #pragma unroll
             for (int grp = 0; grp < NGW; ++grp) {
@@ -412,7 +440,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         // step nrows has stored it)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        store_tile(tile + ((nrows - 1) & 1) * kKTile<C>, p0 + rbe - 1, true);
+        store_tile(tile + ((nrows - 1) & 1) * kKTile<C>, p0 + rbe - 1, true, nrows & 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
 }
@@ -509,6 +537,7 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     a.ps = ps;
     a.pb = pb;
     a.act = act;
+    a.res = nullptr;
 #define PO2Q_RK1(c, d, e, v, tt, lw)                                                                      \
     if (p.C == c && p.pd == d && epi == e && p.vrx == v && !p.nts) {                                         \
         hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e>), dim3((unsigned)p.blocks), dim3(kThreads + (lw ? 64 : 0)), \
@@ -549,6 +578,34 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
 #undef PO2Q_RK1
 #undef PO2Q_RKN
     return hipErrorInvalidValue;
+}
+
+// The residual add inside the kernel: the loader-wave plans of C = K = 32 (po2q_epi.h).
+bool rowsk_res_ok(const ConvPlan& p) {
+    return p.kind == KIND_BF16X3_ROWS && p.vrx == 3 && p.C == 32 && p.K == 32 && p.pd == 3;
+}
+
+hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
+                                 int act, hipStream_t s) {
+    if (!rowsk_res_ok(p) || !res) return hipErrorInvalidValue;
+    RowsKArgs a;
+    a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
+    a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
+    a.items = p.N * p.tilesP * p.tilesQ;
+    a.remap = (p.blocks % 8 == 0) ? 1 : 0;
+    a.ps = ps;
+    a.pb = pb;
+    a.act = act;
+    a.res = res;
+    const size_t lds = p.lds_bytes + 2 * kKTile<32>;
+    if (p.nts)
+        hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, true, true>), dim3((unsigned)p.blocks),
+                           dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    else
+        hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, false, true>), dim3((unsigned)p.blocks),
+                           dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    return hipGetLastError();
 }
 
 }  // namespace po2q

@@ -27,6 +27,11 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 
 // Row-streaming kernels with the affine map + activation in their store epilogue
 // (po2q_conv_rows.hip / po2q_conv_rowsk.hip); the residual is left to launch_epilogue.
+// the residual add in the kernel too (loader-wave plans, po2q_conv_rowsk.hip)
+bool rowsk_res_ok(const ConvPlan& p);
+hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
+                                 int act, hipStream_t s);
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s);
