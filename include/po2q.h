@@ -111,8 +111,8 @@ int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y
  * post_scale / post_shift may be NULL (identity), residual may be NULL; residual is
  * [N, K, P, Q] like y and must not alias y (nor may x).  act: enum po2q_act.  Same
  * workspace as po2q_qconv2d_f32.  The row-streaming kernels apply the affine map and
- * the activation in their store epilogue; other plans and the residual add run one
- * extra elementwise pass over y.
+ * the activation in their store epilogue (the C = K = 32 loader-wave plans the residual
+ * add too); other plans and other residual adds run one extra elementwise pass over y.
  */
 enum po2q_act { PO2Q_ACT_NONE = 0, PO2Q_ACT_RELU = 1, PO2Q_ACT_RELU6 = 2, PO2Q_ACT_SILU = 3 };
 
