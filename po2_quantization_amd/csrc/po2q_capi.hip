@@ -191,9 +191,9 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         bool fused_affine = false;
         if (p.kind == KIND_BF16X3_DMA) {
             he = launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s);
-        } else if (p.kind == KIND_BF16X3_ROWS && e.res && rowsk_res_ok(p)) {
+        } else if (p.kind == KIND_BF16X3_ROWS && e.res && rows_res_ok(p)) {
             // affine, residual and activation all in the kernel's stores
-            st = hip_status(launch_conv_rowsk_res(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s),
+            st = hip_status(launch_conv_rows_res(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s),
                             "conv launch");
             return st;
         } else if (p.kind == KIND_BF16X3_ROWS && e.any()) {

@@ -58,6 +58,7 @@ struct RowsArgs {
     const float* ps;  // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
     const float* pb;
     int act;
+    const float* res;  // RES: y = act(y * ps + pb + res), res [N, K, P, Q]
 };
 
 constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x SW = 512 floats)
@@ -66,8 +67,10 @@ constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): timing ablation bits -- 1 no MFMA,
 // 2 no split (raw bits to the planes), 4 no x loads, 8 no stores, 16 nt stores.  Product:
 // DBG = 0.  NTS: output stores with the non-temporal policy (an autotune candidate).
-template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false>
-__global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const float* __restrict__ x,
+// RES (CC = 16, EPI): the residual add inside the kernel -- each step loads (to VGPRs) the
+// residual of the row the NEXT step stores, so a counted wait finds it landed.
+template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false, bool RES = false>
+__global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(const float* __restrict__ x,
                                                                      const uint4* __restrict__ wpk,
                                                                      const float* __restrict__ scale_p,
                                                                      const float* __restrict__ bias,
@@ -109,7 +112,9 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
     // scaled accumulator -> output value (+ fused eval-BN affine and activation)
     auto outv = [&](float accv, int nt) __attribute__((always_inline)) {
         const float v = accv * scale + bk[nt];
-        if constexpr (EPI)
+        if constexpr (EPI && RES)
+            return v * eps_[nt] + epb_[nt];  // the activation follows the residual add
+        else if constexpr (EPI)
             return epi_act(v * eps_[nt] + epb_[nt], a.act);
         else
             return v;
@@ -193,7 +198,26 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
         rows_dma4(rs, voh, base + (uint32_t)kRawInterior);
     };
     constexpr int ST = NG * NT;      // epilogue stores per step (issued every step)
-    constexpr int VMW = 3 + 2 * ST;  // vm ops issued after a row's DMAs when it is split
+    constexpr int RL = RES ? 2 * NT : 0;  // residual loads per step (issued every step)
+    static_assert(!RES || (NG == 2 && NT == 1), "the residual add needs the transposed store path");
+    constexpr int VMW = 3 + 2 * ST + 2 * RL;  // vm ops issued after a row's DMAs when it is split
+    // RES: the residual, per image, and the two 16-byte pieces this lane adds to its stores
+    const int PQr = a.P * a.Q;
+    const __amdgpu_buffer_rsrc_t rres = rows_rsrc(RES ? a.res + (int64_t)n * a.K * PQr : x, RES ? a.K * PQr * 4 : 4);
+    floatx4 rv[RES ? 2 : 1];
+    auto load_res = [&](int orow_next, bool ok) __attribute__((always_inline)) {
+        if constexpr (RES) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = (lane >> 3) + 8 * i, q = q0 + 4 * (lane & 7);
+                const uint32_t vo = (ok && q < a.Q) ? ((uint32_t)c * (uint32_t)PQr + (uint32_t)orow_next * a.Q + q) * 4u
+                                                    : 0x7fffffffu;
+                // a compiler builtin, not asm: the compiler then places the wait before the
+                // first use itself (an asm output counts as defined when the asm retires)
+                rv[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rres, (int)vo, 0, 0));
+            }
+        }
+    };
     // output descriptor (per image): dropped stores take an out-of-range voffset
     const __amdgpu_buffer_rsrc_t ry = [&] {
         const uintptr_t yp = reinterpret_cast<uintptr_t>(y + (int64_t)n * a.K * a.P * a.Q);
@@ -287,6 +311,10 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
             // runs; 16-byte blocks XOR-swizzled by channel.  Plane 0's zero slot lies in
             // that window and is re-zeroed after.
             const int ch = lane & 15, g = lane >> 4;
+            if constexpr (RES) {  // this row's residual (loaded last step; only the DMAs of row j+2 are younger)
+                rows_wait<3>();
+                asm volatile("" : "+v"(rv[0]), "+v"(rv[1]));
+            }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
 #pragma unroll
@@ -301,7 +329,11 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const int c = (lane >> 3) + 8 * i, b = lane & 7;
-                    const floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
+                    floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
+                    if constexpr (RES) {
+#pragma unroll
+                        for (int e2 = 0; e2 < 4; ++e2) v[e2] = epi_act(v[e2] + rv[i][e2], a.act);
+                    }
                     const int q = q0 + 4 * b;
                     const uint32_t yo = (uint32_t)(nt * 16 + c) * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + q;
                     rows_store<NTS || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
@@ -324,6 +356,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
                 }
             }
         }
+        load_res(o + 1, j + 1 >= 2 && o + 1 < p0 + rbe);  // the row the next step stores
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp)
 #pragma unroll
@@ -338,10 +371,12 @@ __global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const fl
         if constexpr (!(DBG & 8))
 #pragma unroll
             for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
+        load_res(0, false);
         load_row(1, 1);
         if constexpr (!(DBG & 8))
 #pragma unroll
             for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
+        load_res(0, false);
     }
     // steps past nrows DMA zeros (out of range) and store nothing: at most 5 per item
     for (int j = 0; j < nrows; j += 6) {
@@ -433,10 +468,10 @@ void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vec
     }
 }
 
-template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false>
+template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false, bool RES = false>
 static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, hipStream_t s, const float* ps = nullptr,
-                                const float* pb = nullptr, int act = 0) {
+                                const float* pb = nullptr, int act = 0, const float* res = nullptr) {
     RowsArgs a;
     a.N = p.N; a.C = p.C; a.H = p.H; a.W = p.W; a.K = p.K; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
@@ -448,7 +483,8 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
     a.ps = ps;
     a.pb = pb;
     a.act = act;
-    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    a.res = res;
+    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS, RES>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
@@ -514,6 +550,21 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
     if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
     if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
     return hipErrorInvalidValue;
+}
+
+// The residual add inside the kernel (po2q_epi.h): the per-wave C = K = 16 row kernel
+// and the C = K = 32 loader-wave plans.
+bool rows_res_ok(const ConvPlan& p) {
+    return (p.kind == KIND_BF16X3_ROWS && p.vrx == 0 && p.CC == 16 && p.NT == 1) || rowsk_res_ok(p);
+}
+
+hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                const float* bias, float* y, const float* ps, const float* pb, const float* res,
+                                int act, hipStream_t s) {
+    if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
+    if (!rows_res_ok(p) || !res) return hipErrorInvalidValue;
+    if (p.nts) return launch_rows_t<16, 1, 0, true, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
+    return launch_rows_t<16, 1, 0, true, false, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
 }
 
 }  // namespace po2q

@@ -27,7 +27,12 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 
 // Row-streaming kernels with the affine map + activation in their store epilogue
 // (po2q_conv_rows.hip / po2q_conv_rowsk.hip); the residual is left to launch_epilogue.
-// the residual add in the kernel too (loader-wave plans, po2q_conv_rowsk.hip)
+// the residual add in the kernel too: rows_res_ok / launch_conv_rows_res cover every
+// plan that can (po2q_conv_rows.hip), the rowsk_* pair the loader-wave plans
+bool rows_res_ok(const ConvPlan& p);
+hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                const float* bias, float* y, const float* ps, const float* pb, const float* res,
+                                int act, hipStream_t s);
 bool rowsk_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
