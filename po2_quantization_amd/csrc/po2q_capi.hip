@@ -226,12 +226,13 @@ static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dm
 static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
     snprintf(buf, len,
              "kind=%s CC=%d NT=%d MI=%d NJ=%d vr=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
-             "lds=%zu blocks=%lld waves=%d ov=%d wstream=%d pd=%d%s",
+             "lds=%zu blocks=%lld waves=%d ov=%d wstream=%d pd=%d nts=%d var=%d",
              kKindNames[p.kind], p.CC, p.NT, p.MI, p.NJ, p.vrx, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW,
              p.nchunks, p.kblocks, p.steps, p.lds_bytes, (long long)p.blocks,
              p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4, p.dma_ov,
              p.kind == KIND_BF16X3_DMA ? (p.dma_nw > 0) : (p.nchunks > 1 || p.kblocks > 1),
-             (p.kind == KIND_BF16X3 || (p.kind == KIND_BF16X3_ROWS && p.vrx)) ? p.pd : 0, p.nts ? " nts=1" : "");
+             (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_ROWS) ? p.pd : 0, p.nts,
+             p.kind == KIND_BF16X3_ROWS ? p.PS : 0);
 }
 
 int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,

@@ -274,6 +274,8 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
             if (!(nd && nd[0] == '1')) x3p_candidates(p, dma);
             std::vector<PlanCand> rows;
             rows_candidates(p, mode, bits, fsr, rows);
+            std::stable_sort(rows.begin(), rows.end(),
+                             [](const PlanCand& u, const PlanCand& v) { return u.cost < v.cost; });
             p = (!dma.empty() && prefer_dma(p)) ? dma[0].plan : reg[0].plan;
             // the row-streaming kernels beat both tile kernels on every shape they take
             // (profiles/r01_v9_plan_sweep.jsonl, r01_v10_plan_sweep.jsonl)
@@ -313,7 +315,7 @@ bool make_plan(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int64_t 
     return plan_heuristic(p, mode, bits, fsr, flags, nullptr, nullptr);
 }
 
-constexpr int kTuneRegCands = 6, kTuneDmaCands = 12, kTuneRowsCands = 16;
+constexpr int kTuneRegCands = 6, kTuneDmaCands = 12, kTuneRowsCands = 40;
 
 bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                      int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
@@ -331,7 +333,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             for (const ConvPlan& o : out)
                 dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
                        o.dma_waves == c.dma_waves && o.dma_ov == c.dma_ov &&
-                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts;
+                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS;
             if (!dup) out.push_back(c);
         }
     };

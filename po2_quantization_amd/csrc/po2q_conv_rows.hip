@@ -65,16 +65,23 @@ constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x S
 constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
 
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG): timing ablation bits -- 1 no MFMA,
-// 2 no split (raw bits to the planes), 4 no x loads, 8 no stores, 16 nt stores.  Product:
-// DBG = 0.  NTS: output stores with the non-temporal policy (an autotune candidate).
+// 2 no split (raw bits to the planes), 4 no x loads, 8 no stores, 16 nt stores, 32 no
+// halo-column DMA.  Product:
+// DBG = 0.  NTS (plan field nts, autotune candidates): bit 0 = output stores, bit 1 = x
+// loads (LDS-DMA) with the non-temporal policy.
 // RES (CC = 16, EPI): the residual add inside the kernel -- each step loads (to VGPRs) the
 // residual of the row the NEXT step stores, so a counted wait finds it landed.
-template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false, bool RES = false>
+// PD: halo rows in flight per wave (raw ring slots).  What bounds this kernel is the
+// bytes in flight per CU, and those live in LDS (the DMA targets): PD = 2 at 16 waves per
+// CU keeps 32 rows (64 KiB) in flight, PD = 6 at 8 waves 48 rows.
+template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, bool RES = false, int PD = 2>
 __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(const float* __restrict__ x,
                                                                      const uint4* __restrict__ wpk,
                                                                      const float* __restrict__ scale_p,
                                                                      const float* __restrict__ bias,
                                                                      float* __restrict__ y, RowsArgs a) {
+    static_assert(PD >= 2 && PD <= 6, "raw ring slots");
+    static_assert(!RES || PD == 2, "the in-kernel residual runs the 2-row pipeline");
     constexpr int NG = 32 / CC;       // 16-pixel groups per wave
     constexpr int SW = 16 * NG;       // strip width (output columns)
     constexpr int WC = SW + 2;        // halo columns
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
     uint4* wl = reinterpret_cast<uint4*>(lds);
     for (int e = tid; e < NFR * 64; e += kThreads) wl[e] = wpk[e];
     unsigned char* slab = lds + a.w_bytes + wave * a.slab;
-    unsigned char* raw = slab + 3 * a.plane;  // 2 raw slots
+    unsigned char* raw = slab + 3 * a.plane;  // PD raw slots
     const int zero_off = WC * CC * 2;
     if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * a.plane + zero_off) = make_uint4(0u, 0u, 0u, 0u);
     float bk[NT];
@@ -192,15 +199,18 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
         const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
         const uint32_t vo = (hok && qi_ok) ? vi0 + roff : 0x7fffffffu;
         const uint32_t base = raw_lds + (uint32_t)(sl * kRawSlot);
-        rows_dma16(rs, vo, 0u, base);
-        rows_dma16(rs, vo, soff1, base + 1024u);
+        rows_dma16<(NTS & 2) != 0>(rs, vo, 0u, base);
+        rows_dma16<(NTS & 2) != 0>(rs, vo, soff1, base + 1024u);
         const uint32_t voh = (hok && qh_ok) ? vh0 + roff : 0x7fffffffu;
-        rows_dma4(rs, voh, base + (uint32_t)kRawInterior);
+        if constexpr (!(DBG & 32)) rows_dma4<(NTS & 2) != 0>(rs, voh, base + (uint32_t)kRawInterior);
     };
     constexpr int ST = NG * NT;      // epilogue stores per step (issued every step)
     constexpr int RL = RES ? 2 * NT : 0;  // residual loads per step (issued every step)
     static_assert(!RES || (NG == 2 && NT == 1), "the residual add needs the transposed store path");
-    constexpr int VMW = 3 + 2 * ST + 2 * RL;  // vm ops issued after a row's DMAs when it is split
+    // vm ops issued after a row's DMAs (end of step j - PD: DMA, MFMAs, ST stores) until
+    // the wait of step j: that step's stores, then per step in between 3 DMAs + ST stores
+    // (+ the residual loads); PD = 2: 3 + 2 ST (+ 2 RL)
+    constexpr int VMW = ST + (PD - 1) * (3 + ST) + 2 * RL;
     // RES: the residual, per image, and the two 16-byte pieces this lane adds to its stores
     const int PQr = a.P * a.Q;
     const __amdgpu_buffer_rsrc_t rres = rows_rsrc(RES ? a.res + (int64_t)n * a.K * PQr : x, RES ? a.K * PQr * 4 : 4);
@@ -242,7 +252,8 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
     auto step = [&](auto S_, int j) __attribute__((always_inline)) {
         constexpr int S6 = decltype(S_)::value;
         constexpr int S = S6 % 3;   // accumulator rotation
-        constexpr int RS = S6 % 2;  // raw slot
+        // raw slot of row j (static when PD divides the 6-step unroll)
+        const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
         const unsigned char* rw = raw + RS * kRawSlot;
         if constexpr (!(DBG & 4)) rows_wait<VMW>();
         // split + write this halo row into the planes
@@ -268,8 +279,8 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
                 *reinterpret_cast<uint16_t*>(slab + 2 * a.plane + wa_h) = l16;
             }
         }
-        // prefetch halo row j+2 into the raw slot just split
-        if constexpr (!(DBG & 4)) load_row(RS, j + 2);
+        // prefetch halo row j+PD into the raw slot just split
+        if constexpr (!(DBG & 4)) load_row(RS, j + PD);
         // MFMAs: halo row j feeds output halo-index j+1 (r=0), j (r=1), j-1 (r=2)
         constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
 #pragma unroll
@@ -336,7 +347,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
                     }
                     const int q = q0 + 4 * b;
                     const uint32_t yo = (uint32_t)(nt * 16 + c) * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + q;
-                    rows_store<NTS || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
+                    rows_store<(NTS & 1) != 0 || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
                 }
             }
             if (lane == 0) *reinterpret_cast<uint4*>(slab + zero_off) = make_uint4(0u, 0u, 0u, 0u);
@@ -352,7 +363,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
                     v[1] = outv(acc[D][grp][nt][1], nt);
                     v[2] = outv(acc[D][grp][nt][2], nt);
                     v[3] = outv(acc[D][grp][nt][3], nt);
-                    rows_store<NTS || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    rows_store<(NTS & 1) != 0 || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
             }
         }
@@ -364,19 +375,17 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
     };
 
     if constexpr (!(DBG & 4)) {
-        // rows 0 and 1, each followed by ST dropped stores: the steady-state count of
+        // rows 0 .. PD-1, each followed by ST dropped stores: the steady-state count of
         // vm ops between a row's DMAs and its split holds from the first step on
         const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
-        load_row(0, 0);
-        if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
-        load_res(0, false);
-        load_row(1, 1);
-        if constexpr (!(DBG & 8))
+        for (int r = 0; r < PD; ++r) {
+            load_row(r, r);
+            if constexpr (!(DBG & 8))
 #pragma unroll
-            for (int i = 0; i < ST; ++i) rows_store<NTS || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
-        load_res(0, false);
+                for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0 || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
+            load_res(0, false);
+        }
     }
     // steps past nrows DMA zeros (out of range) and store nothing: at most 5 per item
     for (int j = 0; j < nrows; j += 6) {
@@ -399,10 +408,16 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
 hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
                              int act, bool epi);
+// full-row blocks (po2q_conv_rowsf.hip: C = K = 16, plan vrx = 4)
+void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                             const float* bias, float* y, hipStream_t s, const float* ps, const float* pb, int act,
+                             bool epi);
 
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
     rowsk_candidates(base, mode, bits, fsr, out);
+    rowsf_candidates(base, mode, bits, fsr, out);
     if (mode == 0 || b.groups != 1) return;
     if (bits < 1 || bits > 16) return;
     const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
@@ -429,46 +444,49 @@ void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vec
     p.SB = 2 * p.CC;
     p.plane = p.WW * p.SB + 32;
     const int w_bytes = 3 * p.steps * p.NT * 1024;
-    const int waves = p.CC == 16 ? 16 : 12;  // per CU: 4 / 3 per SIMD (launch bounds)
-    p.lds_bytes = (size_t)w_bytes + 4 * (3 * (size_t)p.plane + 2 * kRawSlot);
-    if (p.lds_bytes * (waves / 4) > 160 * 1024) return;
     p.packed_floats = (int64_t)3 * p.steps * p.NT * 64 * 4;
     p.tilesQ = cdivr(p.Q, p.TQ);
-    // rows per segment: minimise (rounds of resident waves) x (halo rows per item)
-    const int slots = 256 * waves;
-    std::vector<std::pair<double, int>> rbs;
-    for (int rb = 8; rb <= p.P; ++rb) {
-        const int nseg = cdivr(p.P, rb);
-        if (rb != cdivr(p.P, nseg)) continue;  // one RB per segment count
-        const int64_t items = (int64_t)p.N * nseg * p.tilesQ;
-        if (items > INT_MAX / 2) continue;
-        const int64_t rounds = (items + slots - 1) / slots;
-        rbs.push_back({(double)rounds * (rb + 2), rb});
-    }
-    std::sort(rbs.begin(), rbs.end());
-    for (int i = 0; i < (int)rbs.size() && i < 3; ++i) {
-        ConvPlan c = p;
-        c.TP = rbs[i].second;
-        c.tilesP = cdivr(p.P, c.TP);
-        const int64_t items = (int64_t)p.N * c.tilesP * c.tilesQ;
-        c.blocks = ((items + 3) / 4 + 7) / 8 * 8;  // whole XCD rounds (extra waves exit at once)
-        // cost comparable with the other bf16x3 planners (their cost ~ 1.0 + overheads)
-        out.push_back({0.9 + 0.001 * i, c});
-    }
-    // the same with non-temporal output stores (interleaved A/B on stage 1: 4-5 % faster
-    // on some boxes, r01_v14; the autotuner decides)
-    for (int i = 0; i < (int)rbs.size() && i < 3; ++i) {
-        ConvPlan c = p;
-        c.TP = rbs[i].second;
-        c.tilesP = cdivr(p.P, c.TP);
-        const int64_t items = (int64_t)p.N * c.tilesP * c.tilesQ;
-        c.blocks = ((items + 3) / 4 + 7) / 8 * 8;
-        c.nts = 1;
-        out.push_back({0.905 + 0.001 * i, c});
+    const int vgpr_waves = p.CC == 16 ? 16 : 12;  // per CU: 4 / 3 per SIMD (launch bounds)
+    // prefetch depth (raw ring slots): C = 16 also 3 and 6 -- fewer waves per CU (LDS),
+    // more rows in flight
+    std::vector<int> pds = {2};
+    if (p.CC == 16) pds = {2, 3, 6};
+    for (int pd : pds) {
+        ConvPlan q = p;
+        q.pd = pd;
+        q.lds_bytes = (size_t)w_bytes + 4 * (3 * (size_t)p.plane + (size_t)pd * kRawSlot);
+        const int blocks_cu = std::min(vgpr_waves / 4, (int)(160 * 1024 / q.lds_bytes));
+        if (blocks_cu < 1) continue;
+        // rows per segment: minimise (rounds of resident waves) x (halo rows per item)
+        const int slots = 256 * 4 * blocks_cu;
+        std::vector<std::pair<double, int>> rbs;
+        for (int rb = 8; rb <= p.P; ++rb) {
+            const int nseg = cdivr(p.P, rb);
+            if (rb != cdivr(p.P, nseg)) continue;  // one RB per segment count
+            const int64_t items = (int64_t)p.N * nseg * p.tilesQ;
+            if (items > INT_MAX / 2) continue;
+            const int64_t rounds = (items + slots - 1) / slots;
+            rbs.push_back({(double)rounds * (rb + 2), rb});
+        }
+        std::sort(rbs.begin(), rbs.end());
+        // plain and non-temporal output stores (interleaved A/B on stage 1: 4-5 % faster on
+        // some boxes, r01_v14); non-temporal x loads measured slower for this walk
+        // (r02: 0.41 vs 0.36 ms), so none.  The autotuner decides.
+        for (int nts : {0, 1})
+            for (int i = 0; i < (int)rbs.size() && i < (pd == 2 ? 3 : 2); ++i) {
+                ConvPlan c = q;
+                c.TP = rbs[i].second;
+                c.tilesP = cdivr(p.P, c.TP);
+                const int64_t items = (int64_t)p.N * c.tilesP * c.tilesQ;
+                c.blocks = ((items + 3) / 4 + 7) / 8 * 8;  // whole XCD rounds (extra waves exit at once)
+                c.nts = nts;
+                // cost comparable with the other bf16x3 planners (their cost ~ 1.0 + overheads)
+                out.push_back({0.9 + 0.005 * nts + 0.001 * i + (pd == 2 ? 0.0 : 0.002 * pd), c});
+            }
     }
 }
 
-template <int CC, int NT, int DBG = 0, bool EPI = false, bool NTS = false, bool RES = false>
+template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, bool RES = false, int PD = 2>
 static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, hipStream_t s, const float* ps = nullptr,
                                 const float* pb = nullptr, int act = 0, const float* res = nullptr) {
@@ -477,20 +495,40 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
     a.items = p.N * p.tilesP * p.tilesQ;
     a.plane = p.plane;
-    a.slab = 3 * p.plane + 2 * kRawSlot;
+    a.slab = 3 * p.plane + PD * kRawSlot;
+    if (p.pd != PD) return hipErrorInvalidValue;
     a.w_bytes = 3 * p.steps * p.NT * 1024;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
     a.ps = ps;
     a.pb = pb;
     a.act = act;
     a.res = res;
-    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS, RES>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS, RES, PD>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
 
+// (CC, NT) x nts -> instantiation; the planner only emits the variants that fit their
+// register budget without spilling
+template <bool EPI>
+static hipError_t rows_dispatch(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
+                                int act) {
+#define PO2Q_ROWS_NTS(cc, nt, d)                                                                                \
+    if (p.CC == cc && p.NT == nt && p.pd == d) {                                                                 \
+        if (p.nts == 1) return launch_rows_t<cc, nt, 0, EPI, 1, false, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
+        if (p.nts == 0) return launch_rows_t<cc, nt, 0, EPI, 0, false, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
+        return hipErrorInvalidValue;                                                                             \
+    }
+    PO2Q_ROWS_NTS(16, 1, 2) PO2Q_ROWS_NTS(16, 1, 3) PO2Q_ROWS_NTS(16, 1, 6)
+    PO2Q_ROWS_NTS(32, 1, 2) PO2Q_ROWS_NTS(32, 2, 2)
+#undef PO2Q_ROWS_NTS
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                    const float* bias, float* y, hipStream_t s) {
+    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
@@ -511,22 +549,14 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
             PO2Q_ROWS_CASE(1) PO2Q_ROWS_CASE(2) PO2Q_ROWS_CASE(3) PO2Q_ROWS_CASE(4) PO2Q_ROWS_CASE(5)
             PO2Q_ROWS_CASE(6) PO2Q_ROWS_CASE(7) PO2Q_ROWS_CASE(8) PO2Q_ROWS_CASE(9) PO2Q_ROWS_CASE(12)
             PO2Q_ROWS_CASE(13) PO2Q_ROWS_CASE(14) PO2Q_ROWS_CASE(15) PO2Q_ROWS_CASE(16) PO2Q_ROWS_CASE(20)
+            PO2Q_ROWS_CASE(32) PO2Q_ROWS_CASE(35) PO2Q_ROWS_CASE(19) PO2Q_ROWS_CASE(51) PO2Q_ROWS_CASE(48)
 #undef PO2Q_ROWS_CASE
             default: break;
         }
     }
 #endif
     // the planner only emits the variants that fit their register budget without spilling
-    if (p.nts) {
-        if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1, 0, false, true>(p, x, packed, scale, bias, y, s);
-        if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, false, true>(p, x, packed, scale, bias, y, s);
-        if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, false, true>(p, x, packed, scale, bias, y, s);
-        return hipErrorInvalidValue;
-    }
-    if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1>(p, x, packed, scale, bias, y, s);
-    if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1>(p, x, packed, scale, bias, y, s);
-    if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2>(p, x, packed, scale, bias, y, s);
-    return hipErrorInvalidValue;
+    return rows_dispatch<false>(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0);
 }
 
 }  // namespace po2q
@@ -536,26 +566,16 @@ namespace po2q {
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s) {
+    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, ps, pb, act, true);
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true);
-    if (p.nts) {
-        if (p.CC == 16 && p.NT == 1)
-            return launch_rows_t<16, 1, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-        if (p.CC == 32 && p.NT == 1)
-            return launch_rows_t<32, 1, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-        if (p.CC == 32 && p.NT == 2)
-            return launch_rows_t<32, 2, 0, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-        return hipErrorInvalidValue;
-    }
-    if (p.CC == 16 && p.NT == 1) return launch_rows_t<16, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-    if (p.CC == 32 && p.NT == 1) return launch_rows_t<32, 1, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-    if (p.CC == 32 && p.NT == 2) return launch_rows_t<32, 2, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act);
-    return hipErrorInvalidValue;
+    return rows_dispatch<true>(p, x, packed, scale, bias, y, s, ps, pb, act);
 }
 
 // The residual add inside the kernel (po2q_epi.h): the per-wave C = K = 16 row kernel
 // and the C = K = 32 loader-wave plans.
 bool rows_res_ok(const ConvPlan& p) {
-    return (p.kind == KIND_BF16X3_ROWS && p.vrx == 0 && p.CC == 16 && p.NT == 1) || rowsk_res_ok(p);
+    return (p.kind == KIND_BF16X3_ROWS && p.vrx == 0 && p.CC == 16 && p.NT == 1 && p.pd == 2 && p.nts <= 1) ||
+           rowsk_res_ok(p);
 }
 
 hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
@@ -563,8 +583,10 @@ hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_
                                 int act, hipStream_t s) {
     if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
     if (!rows_res_ok(p) || !res) return hipErrorInvalidValue;
-    if (p.nts) return launch_rows_t<16, 1, 0, true, true, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
-    return launch_rows_t<16, 1, 0, true, false, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
+    if (p.pd != 2) return hipErrorInvalidValue;
+    if (p.nts == 1) return launch_rows_t<16, 1, 0, true, 1, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
+    if (p.nts == 0) return launch_rows_t<16, 1, 0, true, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace po2q

@@ -78,7 +78,7 @@ struct RowsKArgs {
 // its slot is refilled with row j + PD after the barrier of step j, so it executes
 // exactly the MFMA waves' barriers: one preamble, one per (whole-triple) step and the
 // TT flush.
-template <int C, int PD, bool TT, bool RES>
+template <int C, int PD, bool TT, bool RES, bool NTL>
 __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const RowsKArgs& a, unsigned char* raw,
                                             unsigned char* resb, int n, int q0, int p0, int nrows, int rbe) {
     constexpr int NI = C / 8 + 1;  // instructions per row: C/8 interior + 1 halo
@@ -115,8 +115,8 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
         const uint32_t vo = (hok && qi_ok) ? vi0 + roff : 0x7fffffffu;
         const uint32_t base = raw_lds + (uint32_t)(sl * kKRawSlot<C>);
 #pragma unroll
-        for (int i = 0; i < C / 8; ++i) rows_dma16(rs, vo, i * 8u * cstride, base + (uint32_t)i * 1024u);
-        rows_dma4(rs, (hok && qh_ok) ? vh0 + roff : 0x7fffffffu, base + (uint32_t)kKRawInt<C>);
+        for (int i = 0; i < C / 8; ++i) rows_dma16<NTL>(rs, vo, i * 8u * cstride, base + (uint32_t)i * 1024u);
+        rows_dma4<NTL>(rs, (hok && qh_ok) ? vh0 + roff : 0x7fffffffu, base + (uint32_t)kKRawInt<C>);
     };
 #pragma unroll
     for (int r = 0; r < PD; ++r) lrow(r, r);
@@ -153,10 +153,11 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 // 32 = TT stores non-temporal, 64 = no wait for the DMAs (vmcnt 31), 128 = no DMA
 // instructions in the loop, 256 = no TT tile LDS traffic.
 // Product builds: DBG = 0.
-// NTS: output stores with the non-temporal policy (autotune candidates, plan field nts)
+// NTS (plan field nts, autotune candidates): bit 0 = output stores, bit 1 = x loads with
+// the non-temporal policy
 // RES (with LW, TT, EPI): the residual add inside the kernel (the loader wave DMAs the
 //     residual rows next to the output tile; act after the add)
-template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, bool NTS = false, bool RES = false>
+template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, int NTS = 0, bool RES = false>
 __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
 
     if constexpr (LW) {
         if (wave == 4) {
-            loader_wave<C, PD, TT, RES>(x, a, raw, resb, n, q0, p0, nrows, rbe);
+            loader_wave<C, PD, TT, RES, (NTS & 2) != 0>(x, a, raw, resb, n, q0, p0, nrows, rbe);
             return;
         }
     }
@@ -277,8 +278,8 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         const uint32_t voh = (hok && qh_ok && !(DBG & 1)) ? vh0 + roff : 0x7fffffffu;
         const uint32_t base = raw_lds + (uint32_t)(sl * RAWS);
 #pragma unroll
-        for (int i = 0; i < DPW; ++i) rows_dma16(rs, vo, i * soff1, base + (uint32_t)(DPW * wave + i) * 1024u);
-        rows_dma4(rs, voh, base + (uint32_t)RAWI + (uint32_t)wave * 256u);
+        for (int i = 0; i < DPW; ++i) rows_dma16<(NTS & 2) != 0>(rs, vo, i * soff1, base + (uint32_t)(DPW * wave + i) * 1024u);
+        rows_dma4<(NTS & 2) != 0>(rs, voh, base + (uint32_t)RAWI + (uint32_t)wave * 256u);
     };
     // vm ops issued after a row's DMAs (step j-PD) until row j is split: that step's
     // stores, then per later step the DMAs of one more row and that step's stores
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                 for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e] + r[e], a.act);
             }
             const uint32_t vo = (uint32_t)c * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + (uint32_t)q;
-            rows_store<NTS || (DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
+            rows_store<(NTS & 1) != 0 || (DBG & 32) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? vo * 4u : 0x7fffffffu, v);
         }
     };
 
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             v[1] = outv(acc[D][grp][1]);
             v[2] = outv(acc[D][grp][2]);
             v[3] = outv(acc[D][grp][3]);
-            rows_store<NTS>(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
+            rows_store<(NTS & 1) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
             acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
     };
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         auto pre = [&](auto R_) __attribute__((always_inline)) {
             load_row(R_, decltype(R_)::value);
 #pragma unroll
-            for (int i = 0; i < NGW; ++i) rows_store<NTS>(ry, 0x7fffffffu, z);
+            for (int i = 0; i < NGW; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
         };
         if constexpr (LW) {
             __builtin_amdgcn_s_barrier();  // the loader has rows 0 .. PD-1 in flight, row 0 landed
@@ -517,11 +518,12 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 d.blocks = (items + 7) / 8 * 8;
                 out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0) + (vrx == vrxs[0] ? 0.0 : 0.02), d});
                 // the default variants (C = 64 direct stores, C = 32 loader wave) also with
-                // non-temporal output stores
-                if ((b.C == 64 && vrx == 1) || (b.C == 32 && vrx == 3)) {
-                    d.nts = 1;
-                    out.push_back({0.905 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), d});
-                }
+                // non-temporal output stores (nts 1), non-temporal x loads (2) or both (3)
+                if ((b.C == 64 && vrx == 1) || (b.C == 32 && vrx == 3))
+                    for (int nts : {1, 2, 3}) {
+                        d.nts = nts;
+                        out.push_back({0.905 + 0.001 * i + 0.0001 * nts + (pd == 2 ? 0.01 : 0.0), d});
+                    }
             }
         }
 }
@@ -544,13 +546,15 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
                            p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);     \
         return hipGetLastError();                                                                            \
     }
-#define PO2Q_RKN(c, d, e, v, tt, lw)                                                                      \
-    if (p.C == c && p.pd == d && epi == e && p.vrx == v && p.nts) {                                          \
-        hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e, 0, true>), dim3((unsigned)p.blocks),                \
+#define PO2Q_RKN1(c, d, e, v, tt, lw, nt)                                                                 \
+    if (p.C == c && p.pd == d && epi == e && p.vrx == v && p.nts == nt) {                                    \
+        hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e, 0, nt>), dim3((unsigned)p.blocks),                  \
                            dim3(kThreads + (lw ? 64 : 0)), p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), \
                            scale, bias, y, a);                                                               \
         return hipGetLastError();                                                                            \
     }
+#define PO2Q_RKN(c, d, e, v, tt, lw) \
+    PO2Q_RKN1(c, d, e, v, tt, lw, 1) PO2Q_RKN1(c, d, e, v, tt, lw, 2) PO2Q_RKN1(c, d, e, v, tt, lw, 3)
 #define PO2Q_RK(c, d, e) PO2Q_RK1(c, d, e, 1, false, false) PO2Q_RK1(c, d, e, 2, true, false)
 #ifdef PO2Q_ROWS_DIAG
     if (const char* dv = getenv("PO2Q_ROWSK_DEBUG")) {
@@ -577,6 +581,7 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
 #undef PO2Q_RK
 #undef PO2Q_RK1
 #undef PO2Q_RKN
+#undef PO2Q_RKN1
     return hipErrorInvalidValue;
 }
 
@@ -599,12 +604,17 @@ hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16
     a.act = act;
     a.res = res;
     const size_t lds = p.lds_bytes + 2 * kKTile<32>;
-    if (p.nts)
-        hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, true, true>), dim3((unsigned)p.blocks),
-                           dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
-    else
-        hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, false, true>), dim3((unsigned)p.blocks),
-                           dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+#define PO2Q_RKR(nt)                                                                                         \
+    if (p.nts == nt) {                                                                                       \
+        hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, nt, true>), dim3((unsigned)p.blocks),      \
+                           dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a); \
+        return hipGetLastError();                                                                            \
+    }
+    PO2Q_RKR(1) PO2Q_RKR(2) PO2Q_RKR(3)
+#undef PO2Q_RKR
+    if (p.nts != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv_rowsk<32, 3, true, true, true, 0, 0, true>), dim3((unsigned)p.blocks),
+                       dim3(kThreads + 64), lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
 

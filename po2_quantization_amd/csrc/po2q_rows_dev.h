@@ -16,18 +16,33 @@ namespace po2q {
 
 // One LDS-DMA wave instruction: lane l's 16 (or 4) bytes at rsrc + voff land at LDS
 // m0 + 16*l (4*l).  `s_waitcnt lgkmcnt(0)` first: earlier reads of the slot being
-// refilled have returned.
+// refilled have returned.  NT: non-temporal (streaming) load policy -- on this
+// layer's once-read activations an nt copy moves the same bytes ~10 % faster
+// (tools/copy_probe.hip, profiles/r02_copy_probe.jsonl).
+template <bool NT = false>
 __device__ __forceinline__ void rows_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
                                            uint32_t lds_addr) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %2, %3 offen lds"
-                 ::"v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
-                 : "memory");
+    if constexpr (NT)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %0, %2, %3 offen nt lds"
+                     ::"v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
+                     : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %0, %2, %3 offen lds"
+                     ::"v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
+                     : "memory");
 }
+template <bool NT = false>
 __device__ __forceinline__ void rows_dma4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_addr) {
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen lds"
-                 ::"v"(voff), "s"(lds_addr), "s"(rs)
-                 : "memory");
+    if constexpr (NT)
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen nt lds"
+                     ::"v"(voff), "s"(lds_addr), "s"(rs)
+                     : "memory");
+    else
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen lds"
+                     ::"v"(voff), "s"(lds_addr), "s"(rs)
+                     : "memory");
 }
 // out-of-range voffset (>= the descriptor's size): the store is dropped, yet counted
 template <bool NTS = false>

@@ -87,6 +87,9 @@ SHAPES = [
     (1, 16, 37, 68, 16, 3, 3, 1, 1, 1, 1),
     (1, 32, 23, 20, 16, 3, 3, 1, 1, 1, 1),
     (2, 32, 1, 12, 32, 3, 3, 1, 1, 1, 1),
+    # full-row blocks (C = K = 16): one-row image, seven waves with a ragged last strip
+    (2, 16, 1, 36, 16, 3, 3, 1, 1, 1, 1),
+    (1, 16, 9, 220, 16, 3, 3, 1, 1, 1, 1),
     # C = K = 64 (output channels across a block's waves): ragged strip, short segment
     (2, 64, 12, 40, 64, 3, 3, 1, 1, 1, 1),
     (1, 64, 3, 8, 64, 3, 3, 1, 1, 1, 1),

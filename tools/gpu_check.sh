@@ -32,11 +32,21 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/pytest_gpu.log || grep -q "failed\|error" gpurun_out/pytest_gpu.log; then
                    echo "stopping: GPU tests did not pass"; exit 1
                fi ;;
+        convtests) run convtests 600 python -u -m pytest tests/test_gpu_conv.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/convtests.log || grep -q "failed\|error" gpurun_out/convtests.log; then
+                   echo "stopping: conv GPU tests did not pass"; exit 1
+               fi ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
+        sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
+        sweep0) run sweep0 600 python tools/tile_sweep.py --shapes 0 --iters 21 ;;
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
+        copyprobe) run copyprobe 300 tools/copy_probe 20 ;;
+        ringprobe) run ringprobe 300 tools/copy_probe 20 1 ;;
+        ringprobe2) run ringprobe2 300 tools/copy_probe 20 2 ;;
+        ringprobe3) run ringprobe3 300 tools/copy_probe 20 3 ;;
         counters) run counters 120 rocprofv3 -L ;;
         traffic) run traffic 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" t1 "conv_x3p|conv_bf16x3" hbm
                  python3 tools/traffic.py gpurun_out/pmc_t1 --algorithmic 1644185600 >> gpurun_out/traffic.log 2>&1 ;;
@@ -52,6 +62,8 @@ for s in $STEPS; do
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;
         pmcd1) run pmcd1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" d1 ;;
         pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;
+        ablate_rows1) run ablate_rows1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_rowsdiag/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 11,8 --var PO2Q_ROWS_DEBUG --values 0,3,32,35,8,4,16,19,51,48 --rounds 5 ;;
+        ablate_rowsf) run ablate_rowsf 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_rowsdiag/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 28 --var PO2Q_ROWSF_DEBUG --values 0,1,2,3,4,8,5,10,11 --rounds 5 ;;
         ablate1) run ablate1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 2,3 ;;
         ablate) run ablate 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \

@@ -34,7 +34,8 @@ def short(desc):
     f = dict(kv.split("=") for kv in desc.split())
     k = ("dma%s%s%s" % (f["waves"], "ov" if f.get("ov") == "1" else "", "" if f.get("wstream") != "0" else "wr")
          if f["kind"] == "bf16x3_dma" else ("reg" if f["kind"] == "bf16x3" else f["kind"]))
-    return "%s NJ=%s vr=%s pd=%s %s" % (k, f["NJ"], f["vr"], f.get("pd", "0"), f["tile"])
+    return "%s NJ=%s vr=%s pd=%s nts=%s var=%s %s" % (k, f["NJ"], f["vr"], f.get("pd", "0"), f.get("nts", "0"),
+                                                      f.get("var", "0"), f["tile"])
 
 
 def main():
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=7)
     ap.add_argument("--shapes", default="all")
+    ap.add_argument("--rounds", type=int, default=3, help="interleaved passes over the plans (median reported)")
+    ap.add_argument("--warm-ms", type=float, default=1500.0, help="GPU warm-up before timing (clock ramp)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     shapes = SHAPES if args.shapes == "all" else [SHAPES[int(i)] for i in args.shapes.split(",")]
@@ -50,10 +53,18 @@ def main():
         w = torch.randn(K, C, R, R, device=dev) * 0.1
         P = (H + 2 * pad - R) // st + 1
         plans = _lib.plans(args.batch, C, H, H, K, R, R, st, pad)
-        res = []
-        for i, d in enumerate(plans):
-            t = timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=i), args.iters)
-            res.append((t, i, short(d)))
+        # warm the GPU up first: the first plans of a cold GPU run at ramping clocks
+        import time
+        t_end = time.time() + args.warm_ms / 1e3
+        while time.time() < t_end:
+            for _ in range(10):
+                _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=0)
+            torch.cuda.synchronize()
+        ts = [[] for _ in plans]
+        for _ in range(args.rounds):  # interleaved, so drift hits every plan alike
+            for i in range(len(plans)):
+                ts[i].append(timeit(lambda: _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=i), args.iters))
+        res = [(sorted(t)[len(t) // 2], i, short(d)) for i, (t, d) in enumerate(zip(ts, plans))]
         _lib.benchmark = True
         _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2")  # autotune
         _lib.benchmark = False
