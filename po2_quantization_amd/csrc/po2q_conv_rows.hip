@@ -58,7 +58,6 @@ struct RowsArgs {
     const float* ps;  // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
     const float* pb;
     int act;
-    const float* res;  // RES: y = act(y * ps + pb + res), res [N, K, P, Q]
 };
 
 constexpr int kRawInterior = 2048;             // [C][strip columns] fp32 (C x SW = 512 floats)
@@ -69,19 +68,18 @@ constexpr int kRawSlot = kRawInterior + 256;   // + the halo dwords (64 lanes)
 // halo-column DMA.  Product:
 // DBG = 0.  NTS (plan field nts, autotune candidates): bit 0 = output stores, bit 1 = x
 // loads (LDS-DMA) with the non-temporal policy.
-// RES (CC = 16, EPI): the residual add inside the kernel -- each step loads (to VGPRs) the
-// residual of the row the NEXT step stores, so a counted wait finds it landed.
+// The fused residual add lives in the full-row kernel (po2q_conv_rowsf.hip: residual rows
+// DMA'd into LDS behind the counted row wait); this kernel leaves it to the elementwise pass.
 // PD: halo rows in flight per wave (raw ring slots).  What bounds this kernel is the
 // bytes in flight per CU, and those live in LDS (the DMA targets): PD = 2 at 16 waves per
 // CU keeps 32 rows (64 KiB) in flight, PD = 6 at 8 waves 48 rows.
-template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, bool RES = false, int PD = 2>
-__global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(const float* __restrict__ x,
+template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, int PD = 2>
+__global__ __launch_bounds__(kThreads, CC == 16 ? 4 : 3) void conv_rows(const float* __restrict__ x,
                                                                      const uint4* __restrict__ wpk,
                                                                      const float* __restrict__ scale_p,
                                                                      const float* __restrict__ bias,
                                                                      float* __restrict__ y, RowsArgs a) {
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
-    static_assert(!RES || PD == 2, "the in-kernel residual runs the 2-row pipeline");
     constexpr int NG = 32 / CC;       // 16-pixel groups per wave
     constexpr int SW = 16 * NG;       // strip width (output columns)
     constexpr int WC = SW + 2;        // halo columns
@@ -119,9 +117,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
     // scaled accumulator -> output value (+ fused eval-BN affine and activation)
     auto outv = [&](float accv, int nt) __attribute__((always_inline)) {
         const float v = accv * scale + bk[nt];
-        if constexpr (EPI && RES)
-            return v * eps_[nt] + epb_[nt];  // the activation follows the residual add
-        else if constexpr (EPI)
+        if constexpr (EPI)
             return epi_act(v * eps_[nt] + epb_[nt], a.act);
         else
             return v;
@@ -205,29 +201,9 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
         if constexpr (!(DBG & 32)) rows_dma4<(NTS & 2) != 0>(rs, voh, base + (uint32_t)kRawInterior);
     };
     constexpr int ST = NG * NT;      // epilogue stores per step (issued every step)
-    constexpr int RL = RES ? 2 * NT : 0;  // residual loads per step (issued every step)
-    static_assert(!RES || (NG == 2 && NT == 1), "the residual add needs the transposed store path");
     // vm ops issued after a row's DMAs (end of step j - PD: DMA, MFMAs, ST stores) until
     // the wait of step j: that step's stores, then per step in between 3 DMAs + ST stores
-    // (+ the residual loads); PD = 2: 3 + 2 ST (+ 2 RL)
-    constexpr int VMW = ST + (PD - 1) * (3 + ST) + 2 * RL;
-    // RES: the residual, per image, and the two 16-byte pieces this lane adds to its stores
-    const int PQr = a.P * a.Q;
-    const __amdgpu_buffer_rsrc_t rres = rows_rsrc(RES ? a.res + (int64_t)n * a.K * PQr : x, RES ? a.K * PQr * 4 : 4);
-    floatx4 rv[RES ? 2 : 1];
-    auto load_res = [&](int orow_next, bool ok) __attribute__((always_inline)) {
-        if constexpr (RES) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int c = (lane >> 3) + 8 * i, q = q0 + 4 * (lane & 7);
-                const uint32_t vo = (ok && q < a.Q) ? ((uint32_t)c * (uint32_t)PQr + (uint32_t)orow_next * a.Q + q) * 4u
-                                                    : 0x7fffffffu;
-                // a compiler builtin, not asm: the compiler then places the wait before the
-                // first use itself (an asm output counts as defined when the asm retires)
-                rv[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rres, (int)vo, 0, 0));
-            }
-        }
-    };
+    constexpr int VMW = ST + (PD - 1) * (3 + ST);
     // output descriptor (per image): dropped stores take an out-of-range voffset
     const __amdgpu_buffer_rsrc_t ry = [&] {
         const uintptr_t yp = reinterpret_cast<uintptr_t>(y + (int64_t)n * a.K * a.P * a.Q);
@@ -322,10 +298,6 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
             // runs; 16-byte blocks XOR-swizzled by channel.  Plane 0's zero slot lies in
             // that window and is re-zeroed after.
             const int ch = lane & 15, g = lane >> 4;
-            if constexpr (RES) {  // this row's residual (loaded last step; only the DMAs of row j+2 are younger)
-                rows_wait<3>();
-                asm volatile("" : "+v"(rv[0]), "+v"(rv[1]));
-            }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
 #pragma unroll
@@ -340,11 +312,7 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const int c = (lane >> 3) + 8 * i, b = lane & 7;
-                    floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
-                    if constexpr (RES) {
-#pragma unroll
-                        for (int e2 = 0; e2 < 4; ++e2) v[e2] = epi_act(v[e2] + rv[i][e2], a.act);
-                    }
+                    const floatx4 v = *reinterpret_cast<const floatx4*>(slab + c * 128 + 16 * (b ^ (c & 7)));
                     const int q = q0 + 4 * b;
                     const uint32_t yo = (uint32_t)(nt * 16 + c) * (uint32_t)PQ + (uint32_t)(orow ? o : 0) * a.Q + q;
                     rows_store<(NTS & 1) != 0 || (DBG & 16) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
@@ -367,7 +335,6 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
                 }
             }
         }
-        load_res(o + 1, j + 1 >= 2 && o + 1 < p0 + rbe);  // the row the next step stores
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp)
 #pragma unroll
@@ -384,7 +351,6 @@ __global__ __launch_bounds__(kThreads, CC == 16 && !RES ? 4 : 3) void conv_rows(
             if constexpr (!(DBG & 8))
 #pragma unroll
                 for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0 || (DBG & 16) != 0>(ry, 0x7fffffffu, z);
-            load_res(0, false);
         }
     }
     // steps past nrows DMA zeros (out of range) and store nothing: at most 5 per item
@@ -413,6 +379,10 @@ void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
 hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb, int act,
                              bool epi);
+bool rowsf_res_ok(const ConvPlan& p);
+hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
+                                 int act, hipStream_t s);
 
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
@@ -486,10 +456,10 @@ void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vec
     }
 }
 
-template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, bool RES = false, int PD = 2>
+template <int CC, int NT, int DBG = 0, bool EPI = false, int NTS = 0, int PD = 2>
 static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, hipStream_t s, const float* ps = nullptr,
-                                const float* pb = nullptr, int act = 0, const float* res = nullptr) {
+                                const float* pb = nullptr, int act = 0) {
     RowsArgs a;
     a.N = p.N; a.C = p.C; a.H = p.H; a.W = p.W; a.K = p.K; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
@@ -502,8 +472,7 @@ static hipError_t launch_rows_t(const ConvPlan& p, const float* x, const uint16_
     a.ps = ps;
     a.pb = pb;
     a.act = act;
-    a.res = res;
-    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS, RES, PD>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
+    hipLaunchKernelGGL((conv_rows<CC, NT, DBG, EPI, NTS, PD>), dim3((unsigned)p.blocks), dim3(kThreads), p.lds_bytes, s, x,
                        reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
     return hipGetLastError();
 }
@@ -516,8 +485,8 @@ static hipError_t rows_dispatch(const ConvPlan& p, const float* x, const uint16_
                                 int act) {
 #define PO2Q_ROWS_NTS(cc, nt, d)                                                                                \
     if (p.CC == cc && p.NT == nt && p.pd == d) {                                                                 \
-        if (p.nts == 1) return launch_rows_t<cc, nt, 0, EPI, 1, false, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
-        if (p.nts == 0) return launch_rows_t<cc, nt, 0, EPI, 0, false, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
+        if (p.nts == 1) return launch_rows_t<cc, nt, 0, EPI, 1, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
+        if (p.nts == 0) return launch_rows_t<cc, nt, 0, EPI, 0, d>(p, x, packed, scale, bias, y, s, ps, pb, act); \
         return hipErrorInvalidValue;                                                                             \
     }
     PO2Q_ROWS_NTS(16, 1, 2) PO2Q_ROWS_NTS(16, 1, 3) PO2Q_ROWS_NTS(16, 1, 6)
@@ -571,21 +540,16 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
     return rows_dispatch<true>(p, x, packed, scale, bias, y, s, ps, pb, act);
 }
 
-// The residual add inside the kernel (po2q_epi.h): the per-wave C = K = 16 row kernel
-// and the C = K = 32 loader-wave plans.
-bool rows_res_ok(const ConvPlan& p) {
-    return (p.kind == KIND_BF16X3_ROWS && p.vrx == 0 && p.CC == 16 && p.NT == 1 && p.pd == 2 && p.nts <= 1) ||
-           rowsk_res_ok(p);
-}
+// The residual add inside the kernel (po2q_epi.h): the full-row plans (C = K = 16 / 32,
+// residual rows DMA'd into LDS behind the row wait) and the C = K = 32 loader-wave plans.
+// The per-wave row kernel leaves it to the elementwise pass.
+bool rows_res_ok(const ConvPlan& p) { return rowsf_res_ok(p) || rowsk_res_ok(p); }
 
 hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
                                 int act, hipStream_t s) {
+    if (rowsf_res_ok(p)) return launch_conv_rowsf_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
     if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
-    if (!rows_res_ok(p) || !res) return hipErrorInvalidValue;
-    if (p.pd != 2) return hipErrorInvalidValue;
-    if (p.nts == 1) return launch_rows_t<16, 1, 0, true, 1, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
-    if (p.nts == 0) return launch_rows_t<16, 1, 0, true, 0, true>(p, x, packed, scale, bias, y, s, ps, pb, act, res);
     return hipErrorInvalidValue;
 }
 

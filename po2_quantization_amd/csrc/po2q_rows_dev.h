@@ -1,10 +1,12 @@
 // Device helpers shared by the row-streaming bf16x3 conv kernels
 // (po2q_conv_rows.hip, po2q_conv_rowsk.hip).  Not part of the C ABI.
 //
-// Every global access inside their row loops is inline asm, so hipcc's vmcnt
-// bookkeeping (which at a loop header falls back to vmcnt(0), i.e. waits for every
-// store and every prefetch) stays out of the picture: each step waits with one
-// exact count.
+// Every global access inside their row loops is inline asm (no compiler-visible load or
+// store there), so hipcc's vmcnt bookkeeping -- which at a loop header falls back to
+// vmcnt(0), i.e. waits for every store and every prefetch, and which would place a
+// vmcnt(0) before the first use of any builtin load issued behind asm DMAs -- stays out of
+// the picture: each step waits with one exact, hand-counted `s_waitcnt vmcnt`.  Residual
+// rows go through LDS by the same counted DMAs (po2q_conv_rowsf.hip, po2q_conv_rowsk.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -41,6 +41,7 @@ for s in $STEPS; do
         sweep) run sweep 900 python tools/tile_sweep.py ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep0) run sweep0 600 python tools/tile_sweep.py --shapes 0 --iters 21 ;;
+        sweep3) run sweep3 600 python tools/tile_sweep.py --shapes 3 --iters 21 ;;
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
         copyprobe) run copyprobe 300 tools/copy_probe 20 ;;
@@ -64,6 +65,7 @@ for s in $STEPS; do
         pmcd2) run pmcd2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" d2 ;;
         ablate_rows1) run ablate_rows1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_rowsdiag/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 11,8 --var PO2Q_ROWS_DEBUG --values 0,3,32,35,8,4,16,19,51,48 --rounds 5 ;;
         ablate_rowsf) run ablate_rowsf 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_rowsdiag/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 28 --var PO2Q_ROWSF_DEBUG --values 0,1,2,3,4,8,5,10,11 --rounds 5 ;;
+        ablate_rowsf2) run ablate_rowsf2 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_rowsdiag/libpo2q.so python tools/ablate.py --shape 32,112,32,3,1,1 --plans 0 --var PO2Q_ROWSF_DEBUG --values 0,1,4,8,5,9,12 --rounds 5 ;;
         ablate1) run ablate1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 2,3 ;;
         ablate) run ablate 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
