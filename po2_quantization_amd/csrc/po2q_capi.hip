@@ -155,6 +155,11 @@ static int check_conv_args(const float* x, const float* w, float* y, void* works
     return PO2Q_OK;
 }
 
+static inline void clamp_window_host(int bits, int fsr, int& lo, int& hi) {
+    lo = fsr - (1 << (bits - 1));
+    hi = fsr - 1;
+}
+
 // phases of run_plan: the weight quantize + pack into the workspace, the conv from it
 enum { RUN_PACK = 1, RUN_CONV = 2, RUN_ALL = 3 };
 
@@ -179,7 +184,19 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         if (st) return st;
     }
     if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) {
-        if (phases & RUN_PACK) {
+        // fused weight staging (row plans with fp): the conv quantizes + packs the weight
+        // itself -- one launch, nothing in the workspace
+        WQuant q;
+        if (p.fp) {
+            int lo, hi;
+            clamp_window_host(bits, fsr, lo, hi);
+            q.w = w;
+            q.n = (int)nw;
+            q.lo = lo;
+            q.hi = hi;
+            q.mode = mode - 1;
+        }
+        if ((phases & RUN_PACK) && !p.fp) {
             st = hip_status(launch_pack_bf16x3(p, w, partial, L.nparts, bits, fsr, mode,
                                                reinterpret_cast<uint16_t*>(packed), scale, s),
                             "weight pack launch");
@@ -193,15 +210,15 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
             he = launch_conv_bf16x3_dma(p, x, pk, scale, bias, y, s);
         } else if (p.kind == KIND_BF16X3_ROWS && e.res && rows_res_ok(p)) {
             // affine, residual and activation all in the kernel's stores
-            st = hip_status(launch_conv_rows_res(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s),
+            st = hip_status(launch_conv_rows_res(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s, q),
                             "conv launch");
             return st;
         } else if (p.kind == KIND_BF16X3_ROWS && e.any()) {
             // affine (+ activation unless a residual must be added first) in the kernel
-            he = launch_conv_bf16x3_rows_epi(p, x, pk, scale, bias, y, e.ps, e.pb, e.res ? 0 : e.act, s);
+            he = launch_conv_bf16x3_rows_epi(p, x, pk, scale, bias, y, e.ps, e.pb, e.res ? 0 : e.act, s, q);
             fused_affine = true;
         } else if (p.kind == KIND_BF16X3_ROWS) {
-            he = launch_conv_bf16x3_rows(p, x, pk, scale, bias, y, s);
+            he = launch_conv_bf16x3_rows(p, x, pk, scale, bias, y, s, q);
         } else {
             he = launch_conv_bf16x3(p, x, pk, scale, bias, y, s);
         }
@@ -226,13 +243,13 @@ static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dm
 static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
     snprintf(buf, len,
              "kind=%s CC=%d NT=%d MI=%d NJ=%d vr=%d tile=%dx%d tiles=%dx%d halo=%dx%d chunks=%d kblocks=%d ksteps=%d "
-             "lds=%zu blocks=%lld waves=%d ov=%d wstream=%d pd=%d nts=%d var=%d",
+             "lds=%zu blocks=%lld waves=%d ov=%d wstream=%d pd=%d nts=%d var=%d fp=%d",
              kKindNames[p.kind], p.CC, p.NT, p.MI, p.NJ, p.vrx, p.TP, p.TQ, p.tilesP, p.tilesQ, p.HH, p.WW,
              p.nchunks, p.kblocks, p.steps, p.lds_bytes, (long long)p.blocks,
              p.kind == KIND_BF16X3_DMA ? p.dma_waves : 4, p.dma_ov,
              p.kind == KIND_BF16X3_DMA ? (p.dma_nw > 0) : (p.nchunks > 1 || p.kblocks > 1),
              (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_ROWS) ? p.pd : 0, p.nts,
-             p.kind == KIND_BF16X3_ROWS ? p.PS : 0);
+             p.kind == KIND_BF16X3_ROWS ? p.PS : 0, p.fp);
 }
 
 int po2q_qconv2d_f32(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
@@ -379,6 +396,16 @@ static int pick_plan(ConvPlan& p, int index, int64_t N, int64_t C, int64_t H, in
     return PO2Q_OK;
 }
 
+// The two-enqueue form stages the weight in the workspace: a plan with fused weight
+// staging (fp) runs as its pre-packed twin (same kernel otherwise, also a candidate).
+static int pick_split_plan(ConvPlan& p, int index, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                           int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                           int64_t groups, int mode, int bits, int fsr, int flags) {
+    const int st = pick_plan(p, index, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags);
+    p.fp = 0;
+    return st;
+}
+
 int po2q_qconv2d_pack_f32(int plan, const float* w, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
                           int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
                           int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags,
@@ -387,8 +414,8 @@ int po2q_qconv2d_pack_f32(int plan, const float* w, int64_t N, int64_t C, int64_
     int st = check_conv_args(w, w, const_cast<float*>(w), workspace, mode, bits, flags);
     if (st) return st;
     ConvPlan p;
-    st = pick_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits,
-                   fsr, flags);
+    st = pick_split_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags);
     if (st) return st;
     return run_plan(p, nullptr, w, nullptr, nullptr, bits, fsr, mode, workspace, workspace_bytes,
                     reinterpret_cast<hipStream_t>(stream), ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_PACK);
@@ -402,8 +429,8 @@ int po2q_qconv2d_packed_f32(int plan, const float* x, const float* bias, float* 
     int st = check_conv_args(x, x, y, const_cast<void*>(workspace), mode, bits, flags);
     if (st) return st;
     ConvPlan p;
-    st = pick_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode, bits,
-                   fsr, flags);
+    st = pick_split_plan(p, plan, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups, mode,
+                         bits, fsr, flags);
     if (st) return st;
     return run_plan(p, x, nullptr, bias, y, bits, fsr, mode, const_cast<void*>(workspace), workspace_bytes,
                     reinterpret_cast<hipStream_t>(stream), ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_CONV);

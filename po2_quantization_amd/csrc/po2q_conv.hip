@@ -215,7 +215,7 @@ static bool plan_geometry(ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t 
     p.groups = (int)groups; p.P = (int)P; p.Q = (int)Q; p.Cg = (int)(C / groups); p.Kg = (int)(K / groups);
 
     p.NT = 0; p.SB = 0; p.plane = 0; p.taps = p.R * p.S; p.vrx = 0;
-    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0; p.dma_ov = 0; p.pd = 0; p.nts = 0;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = 0; p.dma_waves = 0; p.dma_ov = 0; p.pd = 0; p.nts = 0; p.fp = 0;
     return true;
 }
 
@@ -333,7 +333,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             for (const ConvPlan& o : out)
                 dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
                        o.dma_waves == c.dma_waves && o.dma_ov == c.dma_ov &&
-                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS;
+                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS && o.fp == c.fp;
             if (!dup) out.push_back(c);
         }
     };

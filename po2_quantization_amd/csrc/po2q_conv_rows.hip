@@ -378,11 +378,11 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
 void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
 hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb, int act,
-                             bool epi);
+                             bool epi, const WQuant& q);
 bool rowsf_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                 int act, hipStream_t s);
+                                 int act, hipStream_t s, const WQuant& q);
 
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
@@ -496,8 +496,9 @@ static hipError_t rows_dispatch(const ConvPlan& p, const float* x, const uint16_
 }
 
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
-                                   const float* bias, float* y, hipStream_t s) {
-    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
+                                   const float* bias, float* y, hipStream_t s, const WQuant& q) {
+    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false, q);
+    if (p.fp) return hipErrorInvalidValue;  // fused weight staging: full-row plans only
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
@@ -534,8 +535,9 @@ namespace po2q {
 
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
-                                       const float* pb, int act, hipStream_t s) {
-    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, ps, pb, act, true);
+                                       const float* pb, int act, hipStream_t s, const WQuant& q) {
+    if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, ps, pb, act, true, q);
+    if (p.fp) return hipErrorInvalidValue;
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true);
     return rows_dispatch<true>(p, x, packed, scale, bias, y, s, ps, pb, act);
 }
@@ -547,8 +549,9 @@ bool rows_res_ok(const ConvPlan& p) { return rowsf_res_ok(p) || rowsk_res_ok(p);
 
 hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                int act, hipStream_t s) {
-    if (rowsf_res_ok(p)) return launch_conv_rowsf_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
+                                int act, hipStream_t s, const WQuant& q) {
+    if (rowsf_res_ok(p)) return launch_conv_rowsf_res(p, x, packed, scale, bias, y, ps, pb, res, act, s, q);
+    if (p.fp) return hipErrorInvalidValue;
     if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
     return hipErrorInvalidValue;
 }

@@ -22,6 +22,9 @@
 //     before this barrier) is refilled right after it -- PD - 1 rows stay in flight.
 //   * RES (fused residual add): each wave DMAs the residual of its own strip for the row
 //     it will store PD - 1 steps later into a wave-private ring, behind the same wait.
+//   * FP (fused weight staging, plan field fp): the block reduces max|w| and quantizes +
+//     packs its B fragments itself (po2q_quant_dev.h wq_*), so the layer is ONE launch --
+//     the reference's quantize-then-conv (quantized_conv.py:35-36) without the pack kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,6 +35,7 @@
 
 #include "po2q_epi.h"
 #include "po2q_internal.h"
+#include "po2q_quant_dev.h"
 #include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
 
@@ -44,6 +48,7 @@ template <int CC> constexpr int kFPlane = kFWC<CC> * CC * 2 + 32;     // bf16 pl
 template <int CC> constexpr int kFKS = CC == 16 ? 2 : 3;              // k-steps per tap row
 template <int CC> constexpr int kFWBytes = 3 * kFKS<CC> * (CC / 16) * 1024;  // B fragments
 constexpr int kFResSlot = 2048;  // residual of one wave's strip and row: [C][SW] fp32
+constexpr int64_t kFusedStageMax = 65536;  // fp plans: every block re-reads the weight from L2
 }  // namespace
 
 struct RowsFArgs {
@@ -55,6 +60,7 @@ struct RowsFArgs {
     const float* pb;
     int act;
     const float* res;  // RES: residual [N, K, P, Q]
+    WQuant q;          // FP: raw weights + quantizer parameters
 };
 
 // PD: raw ring slots (PD - 1 rows in flight ahead of the one being split).
@@ -68,7 +74,7 @@ struct RowsFArgs {
 // DBG (diagnostic builds only, -DPO2Q_ROWS_DIAG, PO2Q_ROWSF_DEBUG; timing only, outputs
 // wrong): 1 = no split and no MFMAs, 2 = no transpose (stores straight from registers),
 // 4 = no x DMAs, 8 = stores dropped (still issued, out of range).  Product: DBG = 0.
-template <int CC, int PD, bool EPI, int NTS, int V = 0, bool RES = false, int DBG = 0>
+template <int CC, int PD, bool EPI, int NTS, int V = 0, bool RES = false, int DBG = 0, bool FP = false>
 __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                      const float* __restrict__ scale_p,
                                                      const float* __restrict__ bias, float* __restrict__ y,
@@ -92,28 +98,12 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
     unsigned char* resr = raw + PD * rawslot + nw * (3 * PL) + wave * (PD * kFResSlot);  // RES ring
     const int zero_off = WC * CC * 2;
 
-    for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x) wl[e] = wpk[e];
-    if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+    // per-lane epilogue parameters and (V & 1) weight fragments: set by the staging below,
+    // after the first row DMAs are on their way
+    float scale = 1.0f;
+    bool fin = true;
     float bk[NT], eps_[NT], epb_[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int k = nt * 16 + (lane & 15);
-        bk[nt] = bias ? bias[k] : 0.0f;
-        eps_[nt] = (EPI && a.ps) ? a.ps[k] : 1.0f;
-        epb_[nt] = (EPI && a.pb) ? a.pb[k] : 0.0f;
-    }
-    const float scale = *scale_p;
     bf16x8 bwr[(V & 1) ? 3 * KS * NT : 1];
-    if constexpr (V & 1) {
-#pragma unroll
-        for (int f = 0; f < 3 * KS * NT; ++f) {
-            bwr[f] = __builtin_bit_cast(bf16x8, wpk[f * 64 + lane]);
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bwr[f]));
-        }
-    }
-    // the parameter loads land here (tied), not at their first use inside the row loop
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bk[nt]), "+v"(eps_[nt]), "+v"(epb_[nt]));
     // accumulator -> output value; with RES the activation follows the residual add
     auto outv = [&](float accv, int nt) __attribute__((always_inline)) {
         const float v = accv * scale + bk[nt];
@@ -124,7 +114,6 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
         else
             return v;
     };
-    __syncthreads();
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -353,6 +342,52 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
             for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
         }
     }
+    // ---- weights, staged while those DMAs fly: fused quantize + pack (FP; scratch in wave
+    // 0's planes, free until its first split) or the pre-packed workspace.  Their loads are
+    // compiler-visible and younger than the DMAs: the waits hipcc places for them are
+    // stricter than the counted row waits, never looser.
+    {
+        unsigned* red = reinterpret_cast<unsigned*>(raw + PD * rawslot);
+        unsigned* thr = red + 16;
+        if constexpr (FP) {
+            scale = wq_prologue(a.q, thr, red, nw, fin);
+            if constexpr (!(V & 1))
+                for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x)
+                    wl[e] = wq_frag_rows(a.q, CC, CC, CC, NT, KS, e, scale, fin, thr);
+        } else {
+            for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x) wl[e] = wpk[e];
+            scale = *scale_p;
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int k = nt * 16 + (lane & 15);
+            bk[nt] = bias ? bias[k] : 0.0f;
+            eps_[nt] = (EPI && a.ps) ? a.ps[k] : 1.0f;
+            epb_[nt] = (EPI && a.pb) ? a.pb[k] : 0.0f;
+        }
+        if constexpr (V & 1) {
+#pragma unroll
+            for (int f = 0; f < 3 * KS * NT; ++f) {
+                if constexpr (FP)
+                    bwr[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q, CC, CC, CC, NT, KS, f * 64 + lane, scale, fin, thr));
+                else
+                    bwr[f] = __builtin_bit_cast(bf16x8, wpk[f * 64 + lane]);
+            }
+        }
+        // every staged value lands here (tied), not at a first use inside the row loop
+        // (that wait would be a vmcnt(0) behind the loop's DMAs and stores)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(bk[nt]), "+v"(eps_[nt]), "+v"(epb_[nt]));
+        if constexpr (V & 1) {
+#pragma unroll
+            for (int f = 0; f < 3 * KS * NT; ++f) asm volatile("" : "+v"(bwr[f]));
+        }
+        // zero slots (own planes; outside the scratch words), then wl and the scratch reads
+        // complete block-wide: wave 0's planes are first written after step 0's barrier
+        if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+    }
     // every wave runs the same steps (block-uniform nrows): the barriers pair up; steps
     // past nrows DMA nothing (out of range) and store nothing
     for (int j = 0; j < nrows; j += 6) {
@@ -430,7 +465,12 @@ void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                     c.blocks = ((int64_t)p.N * c.tilesP + 7) / 8 * 8;
                     c.nts = nts;
                     c.PS = v;
-                    out.push_back({0.89 + 0.001 * i + 0.002 * nts + 0.003 * (pd - 3) + 0.0005 * v, c});
+                    // fused weight staging first (one launch), then the pre-packed form
+                    for (int fp : {1, 0}) {
+                        if (fp && (int64_t)b.K * b.C * 9 > kFusedStageMax) continue;
+                        c.fp = fp;
+                        out.push_back({0.889 + 0.001 * fp + 0.001 * i + 0.002 * nts + 0.003 * (pd - 3) + 0.0005 * v, c});
+                    }
                 }
             }
         }
@@ -442,8 +482,14 @@ static hipError_t launch_rowsf_t(const ConvPlan& p, const RowsFArgs& a, const fl
                                  const float* scale, const float* bias, float* y, hipStream_t s) {
     const int waves = p.TQ / kFSW<CC>;
     const size_t lds = RES ? rowsf_res_lds(p) : p.lds_bytes;
-    hipLaunchKernelGGL((conv_rowsf<CC, PD, EPI, NTS, V, RES, DBG>), dim3((unsigned)p.blocks), dim3(64 * waves), lds, s,
-                       x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    if (p.fp) {
+        if (!a.q.w) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((conv_rowsf<CC, PD, EPI, NTS, V, RES, DBG, true>), dim3((unsigned)p.blocks), dim3(64 * waves),
+                           lds, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    } else {
+        hipLaunchKernelGGL((conv_rowsf<CC, PD, EPI, NTS, V, RES, DBG>), dim3((unsigned)p.blocks), dim3(64 * waves), lds,
+                           s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+    }
     return hipGetLastError();
 }
 
@@ -453,7 +499,8 @@ static bool rowsf_plan_ok(const ConvPlan& p) {
     return waves >= 1 && waves <= 7 && p.TQ == waves * (512 / p.C);
 }
 
-static RowsFArgs rowsf_args(const ConvPlan& p, const float* ps, const float* pb, int act, const float* res) {
+static RowsFArgs rowsf_args(const ConvPlan& p, const float* ps, const float* pb, int act, const float* res,
+                            const WQuant& q) {
     RowsFArgs a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.Wp = p.TQ;
@@ -461,14 +508,15 @@ static RowsFArgs rowsf_args(const ConvPlan& p, const float* ps, const float* pb,
     a.items = p.N * p.tilesP;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
     a.ps = ps; a.pb = pb; a.act = act; a.res = res;
+    a.q = q;
     return a;
 }
 
 hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb, int act,
-                             bool epi) {
+                             bool epi, const WQuant& q) {
     if (!rowsf_plan_ok(p)) return hipErrorInvalidValue;
-    const RowsFArgs a = rowsf_args(p, ps, pb, act, nullptr);
+    const RowsFArgs a = rowsf_args(p, ps, pb, act, nullptr, q);
 #ifdef PO2Q_ROWS_DIAG
     if (const char* dv = getenv("PO2Q_ROWSF_DEBUG")) {
         const int dbg = atoi(dv);
@@ -501,9 +549,9 @@ bool rowsf_res_ok(const ConvPlan& p) { return rowsf_plan_ok(p) && rowsf_res_lds(
 
 hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                 int act, hipStream_t s) {
+                                 int act, hipStream_t s, const WQuant& q) {
     if (!rowsf_res_ok(p) || !res) return hipErrorInvalidValue;
-    const RowsFArgs a = rowsf_args(p, ps, pb, act, res);
+    const RowsFArgs a = rowsf_args(p, ps, pb, act, res, q);
 #define PO2Q_RFR(c, d, nt, v)                            \
     if (p.C == c && p.pd == d && p.nts == nt && p.PS == v) \
         return launch_rowsf_t<c, d, true, nt, v, true>(p, a, x, packed, scale, bias, y, s);

@@ -32,14 +32,14 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 bool rows_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                int act, hipStream_t s);
+                                int act, hipStream_t s, const WQuant& q = WQuant{});
 bool rowsk_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
                                  int act, hipStream_t s);
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
-                                       const float* pb, int act, hipStream_t s);
+                                       const float* pb, int act, hipStream_t s, const WQuant& q = WQuant{});
 
 // One elementwise pass over y [N, K, PQ]: y = act(y * ps[k] + pb[k] + res) (ps / pb
 // skipped when affine_done).

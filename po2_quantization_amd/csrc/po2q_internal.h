@@ -48,6 +48,7 @@ struct ConvPlan {
     int vrx;                     // bf16x3: row-reuse schedule, waves across (0 = generic k-step schedule)
     int pd;                      // bf16x3 register kernel: x prefetch distance in work items (1 or 2)
     int nts;                     // row kernel (vrx 0): non-temporal output stores
+    int fp = 0;                  // row kernels: weights quantized + packed inside the conv (one launch)
     int dma_d0, dma_nck, dma_ni, dma_nw;  // bf16x3 DMA: window offset, 16-B chunks per halo row, DMAs per wave
     int dma_waves;                // bf16x3 DMA: waves per block (4 or 8)
     int dma_ov;                   // bf16x3 DMA: overlapped pipeline (split of item i+1 under the MFMAs of item i)
@@ -69,6 +70,15 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
 
 // Autotune cache: the measured-best plan per problem key (process-wide, thread-safe).
 void tuned_store(const ConvPlan& p, int mode, int bits, int fsr, int flags);
+
+// Fused weight staging source (plan field fp): the raw weight and the quantizer's
+// parameters; w == nullptr selects the pre-packed workspace path.
+struct WQuant {
+    const float* w = nullptr;  // [K, C, 3, 3] fp32
+    int n = 0;                 // weight elements
+    int lo = 0, hi = 0;        // exponent clamp window
+    int mode = 0;              // 0 po2, 1 po2+ (threshold row)
+};
 
 struct PlanCand {
     double cost;  // planner heuristic, lower is better
@@ -106,7 +116,8 @@ hipError_t launch_conv_bf16x3(const ConvPlan& p, const float* x, const uint16_t*
                               const float* scale, const float* bias, float* y, hipStream_t s);
 
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed,
-                                   const float* scale, const float* bias, float* y, hipStream_t s);
+                                   const float* scale, const float* bias, float* y, hipStream_t s,
+                                   const WQuant& q = WQuant{});
 
 hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
                                   const float* scale, const float* bias, float* y, hipStream_t s);

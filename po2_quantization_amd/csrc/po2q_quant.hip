@@ -144,36 +144,6 @@ struct PackX3 {
     int64_t total;  // uint16 elements
 };
 
-__device__ __forceinline__ uint16_t bf16_bits_keep_nan(float q) {
-    const uint32_t u = __float_as_uint(q);
-    const bool nan = ((u & 0x7f800000u) == 0x7f800000u) && (u & 0x007fffffu);
-    return (uint16_t)((u >> 16) | (nan ? 0x40u : 0u));
-}
-
-// W' = Q(w) / scale as bf16 bits: sign(w) * 2^e exactly (fin), else the reference's Q(w).
-// thr: the mode's threshold row staged in LDS (no dependent constant-memory load per
-// weight); same decision as exponent_of (po2q_quant_dev.h).
-__device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, int mode, int lo, int hi,
-                                             const unsigned* thr) {
-    if (fin) {
-        // finite scale: a = |w / scale| <= 1 (w finite; scale = max|w|)
-        const uint32_t b = __float_as_uint(wv / scale) & 0x7fffffffu;
-        int d;
-        if (b == 0u) {
-            d = lo;
-        } else if (b < 0x3f800000u) {
-            const int k = (b >= 0x00800000u) ? (int)(b >> 23) - 127 : (31 - (int)__clz(b)) - 149;
-            d = k + (b >= thr[k - PO2Q_THR_KMIN] ? 1 : 0);
-        } else {
-            d = 0;  // a == 1
-        }
-        const int e = d < lo ? lo : (d > hi ? hi : d);
-        const float sg = ref_sign(wv);
-        return (sg == 0.0f) ? (uint16_t)0 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
-    }
-    return bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
-}
-
 // 1024 threads: the fused absmax (every block reads the whole weight tensor from L2)
 // finishes in one or two rounds of independent loads per thread.
 constexpr int kPackThreads = 1024;

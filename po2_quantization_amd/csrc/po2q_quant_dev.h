@@ -14,6 +14,7 @@
 
 #include <cstdint>
 
+#include "po2q_internal.h"
 #include "po2q_thresholds.h"
 
 namespace po2q {
@@ -74,6 +75,107 @@ __device__ __forceinline__ unsigned block_max_u32(unsigned v, unsigned* red) {
     for (int i = 1; i < NW; ++i) m = red[i] > m ? red[i] : m;
     __syncthreads();
     return m;
+}
+
+__device__ __forceinline__ uint16_t bf16_bits_keep_nan(float q) {
+    const uint32_t u = __float_as_uint(q);
+    const bool nan = ((u & 0x7f800000u) == 0x7f800000u) && (u & 0x007fffffu);
+    return (uint16_t)((u >> 16) | (nan ? 0x40u : 0u));
+}
+
+// W' = Q(w) / scale as bf16 bits: sign(w) * 2^e exactly (fin), else the reference's Q(w).
+// thr: the mode's threshold row staged in LDS (no dependent constant-memory load per
+// weight); same decision as exponent_of (po2q_quant_dev.h).
+__device__ __forceinline__ uint16_t pack_one(float wv, float scale, bool fin, int mode, int lo, int hi,
+                                             const unsigned* thr) {
+    if (fin) {
+        // finite scale: a = |w / scale| <= 1 (w finite; scale = max|w|)
+        const uint32_t b = __float_as_uint(wv / scale) & 0x7fffffffu;
+        int d;
+        if (b == 0u) {
+            d = lo;
+        } else if (b < 0x3f800000u) {
+            const int k = (b >= 0x00800000u) ? (int)(b >> 23) - 127 : (31 - (int)__clz(b)) - 149;
+            d = k + (b >= thr[k - PO2Q_THR_KMIN] ? 1 : 0);
+        } else {
+            d = 0;  // a == 1
+        }
+        const int e = d < lo ? lo : (d > hi ? hi : d);
+        const float sg = ref_sign(wv);
+        return (sg == 0.0f) ? (uint16_t)0 : (uint16_t)(((sg < 0.0f) ? 0x8000u : 0u) | ((unsigned)(e + 127) << 7));
+    }
+    return bf16_bits_keep_nan(quantize_elem(wv, scale, mode, lo, hi));
+}
+
+
+// ---- fused weight staging (row conv kernels, plan field fp): every block reduces
+// max|w| over the whole small, L2-resident weight tensor itself and quantizes + packs
+// the B fragments it needs, so a quantized conv is ONE launch (no pack kernel, no
+// workspace round trip).  Same decision (threshold table), same fragments as
+// pack_bf16x3_kernel (po2q_quant.hip).
+
+// Block-wide max|w| bits (NaN > inf > finite) over nw waves; red: nw LDS words.
+__device__ __forceinline__ unsigned wq_absmax(const float* __restrict__ w, int n, unsigned* red, int nw) {
+    unsigned m = 0u;
+    const int tid = threadIdx.x, nt = (int)blockDim.x;
+    if ((reinterpret_cast<uintptr_t>(w) & 15u) == 0) {
+        const int n4 = n >> 2;
+        const float4* w4 = reinterpret_cast<const float4*>(w);
+        for (int i = tid; i < n4; i += nt) {
+            const float4 v = w4[i];
+            const unsigned a = __float_as_uint(v.x) & 0x7fffffffu, b = __float_as_uint(v.y) & 0x7fffffffu;
+            const unsigned c = __float_as_uint(v.z) & 0x7fffffffu, d = __float_as_uint(v.w) & 0x7fffffffu;
+            m = max(m, max(max(a, b), max(c, d)));
+        }
+        for (int i = (n4 << 2) + tid; i < n; i += nt) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+    } else {
+        for (int i = tid; i < n; i += nt) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+    }
+    m = wave_max_u32(m);
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    unsigned r = red[0];
+    for (int i = 1; i < nw; ++i) r = red[i] > r ? red[i] : r;
+    return r;
+}
+
+// B fragment j of the row layout [r][ks][nt][lane][8] (pack_bf16x3_kernel, vr == 2):
+// CC = 16: ks 0 -> k < 16: s = 0, k >= 16: s = 1; ks 1 -> k < 16: s = 2, else 0.
+// CC = 32: ks = chunk * 3 + s, k = the chunk's 32 channels.
+__device__ __forceinline__ uint4 wq_frag_rows(const WQuant& q, int C, int K, int CC, int NT, int ksteps, int j,
+                                              float scale, bool fin, const unsigned* thr) {
+    const int lane = j & 63, t = j >> 6;
+    const int nt = t % NT;
+    const int ks = (t / NT) % ksteps;
+    const int r = t / (NT * ksteps);
+    const int grp = lane >> 4;
+    int sft, c0;
+    if (CC == 16) {
+        sft = ks == 0 ? (grp >> 1) : (grp < 2 ? 2 : -1);
+        c0 = 8 * (grp & 1);
+    } else {
+        sft = ks % 3;
+        c0 = (ks / 3) * 32 + 8 * grp;
+    }
+    const int k = nt * 16 + (lane & 15);
+    const bool ok = k < K && sft >= 0;
+    uint32_t h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        h[e] = (ok && c < C) ? pack_one(q.w[(k * C + c) * 9 + r * 3 + sft], scale, fin, q.mode, q.lo, q.hi, thr) : 0u;
+    }
+    return make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+}
+
+// Stage the threshold row (LDS) and reduce the scale; returns the conv's multiplier
+// (max|w|, or 1 where the reference's Q(w) itself is packed).  thr: PO2Q_THR_COUNT LDS
+// words, red: nw LDS words.  Ends with the block's threshold row visible to every thread.
+__device__ __forceinline__ float wq_prologue(const WQuant& q, unsigned* thr, unsigned* red, int nw, bool& fin) {
+    for (int i = threadIdx.x; i < PO2Q_THR_COUNT; i += blockDim.x) thr[i] = po2q_thr[q.mode > 0 ? 1 : 0][i];
+    const unsigned m = wq_absmax(q.w, q.n, red, nw);  // its barrier also publishes thr
+    fin = (m > 0u) && (m < 0x7f800000u);
+    return fin ? __uint_as_float(m) : 1.0f;
 }
 
 }  // namespace po2q

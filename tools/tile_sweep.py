@@ -34,8 +34,8 @@ def short(desc):
     f = dict(kv.split("=") for kv in desc.split())
     k = ("dma%s%s%s" % (f["waves"], "ov" if f.get("ov") == "1" else "", "" if f.get("wstream") != "0" else "wr")
          if f["kind"] == "bf16x3_dma" else ("reg" if f["kind"] == "bf16x3" else f["kind"]))
-    return "%s NJ=%s vr=%s pd=%s nts=%s var=%s %s" % (k, f["NJ"], f["vr"], f.get("pd", "0"), f.get("nts", "0"),
-                                                      f.get("var", "0"), f["tile"])
+    return "%s NJ=%s vr=%s pd=%s nts=%s var=%s fp=%s %s" % (k, f["NJ"], f["vr"], f.get("pd", "0"), f.get("nts", "0"),
+                                                            f.get("var", "0"), f.get("fp", "0"), f["tile"])
 
 
 def main():
