@@ -13,6 +13,12 @@ on its first (untimed, warmup) call, as the reference's cudnn.benchmark does.
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+  python bench.py --image 32 --graph                     (config 2: CIFAR 32x32, hipGraph replay)
+  torchrun ... bench.py --gpus 8 --global-batch 1024     (config 4: 128 images per GPU)
+
+--graph captures one whole step (every fused quantize+conv launch of the chain + head) in
+a HIP graph after the warm-up / autotune steps and times its replays: at 32x32 a layer is
+a few microseconds of GPU work, less than the host's launch cost.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -20,6 +26,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -148,7 +155,15 @@ def cpu_baseline(layers, weights_cpu, image, mode, bits, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
+    cpu_model = None
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name:"):
+                cpu_model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
     return {"value": round(nb * reps / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model,
             "sample": "%d passes x %d images of the ResNet56 %dx%d quantized-conv chain (oracle quantizer "
                       "+ torch CPU F.conv2d/oneDNN, %d threads), %.1f s" % (reps, nb, image, image, threads, dt)}
 
@@ -192,6 +207,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="images per step over all GPUs (split evenly; overrides --batch)")
+    ap.add_argument("--graph", action="store_true", help="replay the step from a HIP graph")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--model", default="resnet56", choices=["resnet20", "resnet32", "resnet44", "resnet56"])
     ap.add_argument("--classes", type=int, default=1000)
@@ -217,6 +235,10 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    if args.global_batch is not None:
+        if args.global_batch % world:
+            raise SystemExit("--global-batch %d is not divisible by the %d ranks" % (args.global_batch, world))
+        args.batch = args.global_batch // world
     n_blocks = {"resnet20": 3, "resnet32": 5, "resnet44": 7, "resnet56": 9}[args.model]
     chain = QConvChain(n_blocks, args.classes, args.quantizer, args.bits, args.precision, dev, seed=0)
     chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
@@ -227,13 +249,52 @@ def main():
     def step(record=False):
         return gather_logits(chain.forward(x, record), gathered, world)
 
+    graph = None
+    if args.graph:
+        with torch.no_grad():
+            for _ in range(max(args.warmup, 1)):  # autotune + warm the caching allocator
+                step()
+            torch.cuda.synchronize()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                chain.forward(x)
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                logits = chain.forward(x)
+        gstep = lambda record=False: gather_logits(graph.replay() or logits, gathered, world)  # noqa: E731
+
     with torch.no_grad():
         # autotuning needs one untimed pass
-        dt = timed_steps(step, args.steps, max(args.warmup, 1 if _lib.benchmark else 0), world,
-                         torch.cuda.synchronize, dev)
+        dt = timed_steps(gstep if graph is not None else step, args.steps,
+                         max(args.warmup, 1 if _lib.benchmark else 0), world, torch.cuda.synchronize, dev)
 
     # dominant op: fused quantize+conv of the timed shape, HIP events on its stream
-    ev_ms = [a.elapsed_time(b) for a, b in chain.events]
+    if graph is not None:
+        # per-launch time from a graph of back-to-back launches of that layer alone
+        with torch.no_grad():
+            _, C0, _, _, _, _, _ = chain.layers[chain.timed_layer]
+            xl = torch.relu(torch.randn(args.batch, C0, args.image, args.image, device=dev))
+            reps = 20
+            chain.conv(chain.timed_layer, xl)
+            torch.cuda.synchronize()
+            lg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(lg):
+                for _ in range(reps):
+                    chain.conv(chain.timed_layer, xl)
+            lg.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                lg.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            chain.events = [(e0, e1)]
+            ev_scale = 1.0 / (5 * reps)
+    else:
+        ev_scale = 1.0
+    ev_ms = [a.elapsed_time(b) * ev_scale for a, b in chain.events]
     avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
     _, C, K, R, st, pad, _ = chain.layers[chain.timed_layer]
     flops, nbytes = conv_work(B, C, Hs, K, R, st, pad)
@@ -278,7 +339,8 @@ def main():
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
-                   "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world},
+                   "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world, "world_size": world,
+                   "hip_graph": graph is not None},
         "roofline": roof,
         "cpu_baseline": None,
     }

@@ -199,6 +199,34 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
                           int64_t dil_h, int64_t dil_w, int64_t groups,
                           int bits, int fsr, int mode, int flags, char* buf, size_t len);
 
+/*
+ * Plan handles: a conv problem resolved ONCE to its kernel plan (the tuned plan when
+ * po2q_qconv2d_autotune has measured it in this process, else the heuristic one; or
+ * candidate `index` >= 0 of po2q_qconv2d_plans), so a framework binding that caches the
+ * handle per problem pays no planning cost per call.  The PyTorch extension
+ * (po2_quantization_amd/csrc/po2q_torch.cpp: torch.ops.po2q.*) keeps one per shape key.
+ *   po2q_qconv2d_plan_create            resolve (same arguments as po2q_qconv2d_f32 + index)
+ *   po2q_qconv2d_plan_workspace_bytes   the workspace THIS plan needs
+ *   po2q_qconv2d_plan_run               quantize + conv (+ the fused epilogue of
+ *                                       po2q_qconv2d_fused_f32: post_scale / post_shift /
+ *                                       residual may be NULL, act PO2Q_ACT_*) on `stream`
+ * Handles are immutable after creation; run may be called concurrently on one handle.
+ * Replaces per call: QuantizedConv2d.forward (models/quantized_conv.py:32-38).
+ */
+typedef struct po2q_conv_plan po2q_conv_plan;
+int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index,
+                             int64_t N, int64_t C, int64_t H, int64_t W,
+                             int64_t K, int64_t R, int64_t S,
+                             int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                             int64_t dil_h, int64_t dil_w, int64_t groups,
+                             int bits, int fsr, int mode, int flags);
+size_t po2q_qconv2d_plan_workspace_bytes(const po2q_conv_plan* plan);
+int po2q_qconv2d_plan_run(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias, float* y,
+                          const float* post_scale, const float* post_shift, const float* residual, int act,
+                          void* workspace, size_t workspace_bytes, void* stream);
+int po2q_qconv2d_plan_describe(const po2q_conv_plan* plan, char* buf, size_t len);
+void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

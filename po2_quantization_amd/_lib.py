@@ -1,10 +1,17 @@
-"""ctypes binding of the po2q C ABI (include/po2q.h) for torch tensors.
+"""Python front end of the po2q native library.
 
-This is the only bridge between Python and the HIP kernels.  Tensors are handed
-over as raw device pointers plus sizes, and launches go onto torch's current
-HIP stream, so the ops compose with torch streams and graph capture.  There is
-deliberately no CPU or torch fallback: a missing library or a non-HIP / non-fp32
-tensor raises.
+The compute path is the PyTorch-ROCm operator library torch.ops.po2q.* (csrc/po2q_torch.cpp,
+built into lib/libpo2q_torch.so by build_ext.py on top of the C ABI include/po2q.h): the
+quantize / qconv2d / qconv2d_fused / quantize_lin ops validate tensors, keep one resolved
+plan handle per conv problem and launch on torch's current HIP stream (they compose with
+torch streams and graph capture).  The ctypes binding of the same C ABI below serves the
+planning / tuning / diagnostic entry points, the two-enqueue SplitConv, and every call when
+PO2Q_LIB points at another build of libpo2q.so (diagnostic builds).
+
+fp32 HIP tensors always run the native kernels: a missing library raises, there is no
+torch fallback for them.  Only the PO2 / PO2+ quantizer accepts other inputs (CPU tensors,
+fp64, bf16, ...): those take restated_quantize, the reference formula written as torch ops
+in the input's own dtype and device (the reference preserves dtype).
 """
 import ctypes
 import os
@@ -12,7 +19,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PO2Q_LIB", os.path.join(_HERE, "lib", "libpo2q.so"))
+_DEFAULT_LIB = os.path.join(_HERE, "lib", "libpo2q.so")
+LIB_PATH = os.environ.get("PO2Q_LIB", _DEFAULT_LIB)
+OPS_PATH = os.path.join(_HERE, "lib", "libpo2q_torch.so")
 
 MODES = {None: 0, "none": 0, "po2": 1, "po2+": 2}
 PRECISIONS = {"auto": 0, "fp32": 1, "bf16x3": 2}
@@ -35,6 +44,11 @@ EXPORTS = (
     "po2q_qconv2d_plans",
     "po2q_qconv2d_f32_plan",
     "po2q_qconv2d_describe",
+    "po2q_qconv2d_plan_create",
+    "po2q_qconv2d_plan_workspace_bytes",
+    "po2q_qconv2d_plan_run",
+    "po2q_qconv2d_plan_describe",
+    "po2q_qconv2d_plan_destroy",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -49,10 +63,35 @@ _tune_file = os.environ.get("PO2Q_TUNE_FILE")
 _tune_db = None
 
 _lib = None
+_ops = None
 
 
 class Po2qError(RuntimeError):
     pass
+
+
+def ops():
+    """torch.ops.po2q, loading lib/libpo2q_torch.so once (raises if it has not been built),
+    or None when PO2Q_LIB selects another libpo2q build (the ops link the default one)."""
+    global _ops
+    if _ops is not None:
+        return _ops
+    if os.path.realpath(LIB_PATH) != os.path.realpath(_DEFAULT_LIB):
+        return None
+    if not os.path.exists(OPS_PATH):
+        raise Po2qError("po2q: operator library %s not found; build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'`" % OPS_PATH)
+    load()  # the same libpo2q.so the ops link (one process-wide plan / tune cache)
+    torch.ops.load_library(OPS_PATH)
+    _ops = torch.ops.po2q
+    return _ops
+
+
+def _op_call(fn, *args, **kwargs):
+    try:
+        return fn(*args, **kwargs)
+    except RuntimeError as e:  # TORCH_CHECK -> RuntimeError; keep the po2q error type
+        raise Po2qError(str(e).split("\nException raised from")[0]) from None
 
 
 def load():
@@ -123,13 +162,41 @@ def _workspace(nbytes, dev):
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
 
 
+def restated_quantize(w, bits, mode, fsr=1):
+    """PO2 / PO2+ for inputs the native kernel does not take (CPU tensors, fp64, bf16, ...):
+    the reference's elementwise formula (utils/quantizers.py:21-32, :41-52) as torch ops in
+    w's own dtype and device -- torch's own log2 / round decide, so the result is the
+    reference's bit for bit in every dtype.  Product code for those inputs only; fp32 HIP
+    tensors always take the native kernel."""
+    scale = torch.max(torch.abs(w))  # (raises for an empty tensor, as the reference does)
+    a = (w / scale).abs()
+    t = torch.log2(a / 1.5) + 0.5 if mode == "po2+" else torch.log2(a)
+    lo, hi = fsr - 2 ** (bits - 1), fsr - 1
+    e = torch.clamp(torch.round(t), lo, hi)
+    # 2**e from a table of exact powers of two (Python floats are exact): a device's
+    # pow(2, e) need not be (it is not for fp64 on the GPU), the CPU reference's is
+    levels = torch.tensor([2.0 ** k for k in range(lo, hi + 1)], dtype=w.dtype, device=w.device)
+    nan = torch.isnan(e)
+    p2 = levels[torch.where(nan, lo, e).long() - lo]
+    p2 = torch.where(nan, e, p2)
+    return p2 * torch.sign(w) * scale
+
+
 def quantize(w, bits, mode, fsr=1):
     """PO2 / PO2+ quantization of a whole tensor (utils/quantizers.py:19-56)."""
-    _require_hip_f32(w, "input")
-    L = load()
+    if not isinstance(w, torch.Tensor):
+        raise TypeError("po2q: input must be a torch.Tensor")
     mode_id = MODES[mode]
     if mode_id == 0:
         raise Po2qError("po2q: quantize() needs mode 'po2' or 'po2+'")
+    if w.device.type != "cuda" or w.dtype != torch.float32:
+        return restated_quantize(w, int(bits), mode, int(fsr))
+    if w.numel() == 0:
+        raise Po2qError("po2q: max(): Expected reduction dim to be specified for input.numel() == 0")
+    O = ops()
+    if O is not None:
+        return _op_call(O.quantize, w, int(bits), mode_id, int(fsr))
+    L = load()
     wc = w.contiguous()
     out = torch.empty_like(wc)
     n = wc.numel()
@@ -147,6 +214,9 @@ def quantize_lin(w, bits, plus, num_iters=10):
     if w.dim() != 4:
         # the reference reduces dims 3, 2, 0 explicitly (torch.max(..., dim=3) ...)
         raise Po2qError("po2q: the lin quantizers need a 4-D weight (got %d dims)" % w.dim())
+    O = ops()
+    if O is not None:
+        return _op_call(O.quantize_lin, w, int(bits), int(num_iters), 1 if plus else 0)
     L = load()
     wc = w.contiguous()
     out = torch.empty_like(wc)
@@ -193,11 +263,20 @@ def qconv2d(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, 
     plan=None runs the tuned (or heuristic) plan, autotuning first when benchmark
     mode is on; plan=i runs candidate i of plans() (tests / tuning tools)."""
     xc, wc, bc, args, yshape = _conv_geometry(x, w, bias, stride, padding, dilation, groups)
-    L = load()
     mode_id = MODES[mode]
     prec = PRECISIONS[precision]
     if yshape[0] == 0:  # an empty batch: torch's F.conv2d returns an empty output
         return torch.empty(yshape, dtype=torch.float32, device=xc.device)
+    O = ops()
+    if O is not None:
+        key = args + (int(bits), int(fsr), mode_id, prec)
+        idx, tune = _plan_choice(key, plan)
+        y = _op_call(O.qconv2d, xc, wc, bc, list(args[7:9]), list(args[9:11]), list(args[11:13]), args[13],
+                     int(bits), mode_id, int(fsr), prec, idx, tune)
+        if tune:
+            _after_tune(key)
+        return y
+    L = load()
     with torch.cuda.device(xc.device):
         nbytes = L.po2q_qconv2d_workspace_bytes(*args, int(bits), int(fsr), mode_id, prec)
         if nbytes == 0:
@@ -238,6 +317,8 @@ def qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bi
     for t, what in ((post_scale, "post_scale"), (post_shift, "post_shift")):
         if t is not None:
             _require_hip_f32(t, what)
+            if t.device != xc.device:
+                raise Po2qError("po2q: %s must be on the input's device" % what)
             if t.numel() != yshape[1]:
                 raise Po2qError("po2q: %s must have %d elements, got %d" % (what, yshape[1], t.numel()))
             t = t.contiguous()
@@ -245,12 +326,24 @@ def qconv2d_fused(x, w, bias=None, stride=1, padding=0, dilation=1, groups=1, bi
     rc = None
     if residual is not None:
         _require_hip_f32(residual, "residual")
+        if residual.device != xc.device:
+            raise Po2qError("po2q: residual must be on the input's device")
         if tuple(residual.shape) != tuple(yshape):
             raise Po2qError("po2q: residual shape %s does not match the output %s"
                             % (list(residual.shape), list(yshape)))
         rc = residual.contiguous()
     if yshape[0] == 0:
         return torch.empty(yshape, dtype=torch.float32, device=xc.device)
+    O = ops()
+    if O is not None:
+        # the saved / tuned plan, exactly as qconv2d runs it (autotuning first if due)
+        key = args + (int(bits), int(fsr), mode_id, prec)
+        idx, tune = _plan_choice(key, None)
+        y = _op_call(O.qconv2d_fused, xc, wc, bc, list(args[7:9]), list(args[9:11]), list(args[11:13]), args[13],
+                     int(bits), mode_id, int(fsr), prec, idx, tune, ext[0], ext[1], rc, ACTS[act])
+        if tune:
+            _after_tune(key)
+        return y
     with torch.cuda.device(xc.device):
         key = args + (int(bits), int(fsr), mode_id, prec)
         nbytes = L.po2q_qconv2d_workspace_bytes(*key)
@@ -315,6 +408,25 @@ class SplitConv:
         _check(load().po2q_qconv2d_packed_f32(self._plan(), xc.data_ptr(), bp, y.data_ptr(), *self.key,
                                               self.ws.data_ptr(), self.ws.numel(), _stream(xc.device)))
         return y
+
+
+def _plan_choice(key, plan):
+    """(plan index for the op, autotune flag): an explicit candidate, the PO2Q_TUNE_FILE
+    record, or -1 (tuned / heuristic) with autotuning on the first call when due."""
+    if plan is not None:
+        return int(plan), 0
+    saved = _saved_plan(key)
+    if saved is not None:
+        return int(saved), 0
+    return -1, 1 if (key not in _tuned and _benchmark_enabled()) else 0
+
+
+def _after_tune(key):
+    _tuned.add(key)
+    if _tune_file:
+        buf = ctypes.create_string_buffer(512)
+        _check(load().po2q_qconv2d_describe(*key, buf, 512))
+        _save_plan(key, buf.value.decode())
 
 
 def _tune_key(key):

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <algorithm>
+#include <new>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -453,3 +454,76 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ plan handles --
+struct po2q_conv_plan {
+    po2q::ConvPlan p;
+    int bits, fsr, mode;
+    size_t ws;
+};
+
+int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
+                             int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                             int64_t dil_h, int64_t dil_w, int64_t groups, int bits, int fsr, int mode, int flags) {
+    using namespace po2q;
+    if (!out) {
+        set_error("po2q: null plan output pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    *out = nullptr;
+    if (!check_mode_bits(mode, bits, true)) return PO2Q_ERR_INVALID;
+    if (flags < PO2Q_PREC_AUTO || flags > PO2Q_PREC_BF16X3) {
+        set_error("po2q: unknown precision flag " + std::to_string(flags));
+        return PO2Q_ERR_INVALID;
+    }
+    ConvPlan p;
+    const int st = pick_plan(p, index, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups,
+                             mode, bits, fsr, flags);
+    if (st) return st;
+    po2q_conv_plan* h = new (std::nothrow) po2q_conv_plan;
+    if (!h) {
+        set_error("po2q: out of host memory");
+        return PO2Q_ERR_INVALID;
+    }
+    h->p = p;
+    h->bits = bits;
+    h->fsr = fsr;
+    h->mode = mode;
+    h->ws = std::max<size_t>(ws_layout(p, mode).total, 256);
+    *out = h;
+    return PO2Q_OK;
+}
+
+size_t po2q_qconv2d_plan_workspace_bytes(const po2q_conv_plan* plan) { return plan ? plan->ws : 0; }
+
+int po2q_qconv2d_plan_run(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias, float* y,
+                          const float* post_scale, const float* post_shift, const float* residual, int act,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace po2q;
+    if (!plan) {
+        set_error("po2q: null plan");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!x || !w || !y || !workspace) {
+        set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (act < PO2Q_ACT_NONE || act > PO2Q_ACT_SILU) {
+        set_error("po2q: unknown activation " + std::to_string(act));
+        return PO2Q_ERR_INVALID;
+    }
+    const ConvEpi e{post_scale, post_shift, residual, act};
+    return run_plan(plan->p, x, w, bias, y, plan->bits, plan->fsr, plan->mode, workspace, workspace_bytes,
+                    reinterpret_cast<hipStream_t>(stream), e);
+}
+
+int po2q_qconv2d_plan_describe(const po2q_conv_plan* plan, char* buf, size_t len) {
+    if (!plan || !buf || len == 0) {
+        po2q::set_error("po2q: null plan or buffer");
+        return PO2Q_ERR_INVALID;
+    }
+    describe_plan(plan->p, buf, len);
+    return PO2Q_OK;
+}
+
+void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan) { delete plan; }

@@ -1,0 +1,276 @@
+// PyTorch-ROCm operator library for po2q: torch.ops.po2q.* registered through
+// TORCH_LIBRARY on top of the C ABI (include/po2q.h, libpo2q.so).  Host C++ only -- every
+// kernel lives in libpo2q.so; this file turns torch tensors into pointers, keeps one
+// resolved plan handle + workspace size per conv problem, and launches on torch's current
+// HIP stream.  Replaces the reference's call sites:
+//   po2q::quantize       PowerOfTwoQuantizer / PowerOfTwoPlusQuantizer.forward
+//                        (utils/quantizers.py:19-56)
+//   po2q::quantize_lin   LinearPowerOfTwo(Plus)Quantizer.forward (utils/quantizers.py:59-136)
+//   po2q::qconv2d        QuantizedConv2d.forward: F.conv2d(x, Q(w), bias, ...)
+//                        (models/quantized_conv.py:32-38)
+//   po2q::qconv2d_fused  the same + eval BatchNorm affine, residual add and activation of
+//                        the blocks (resnet.py:55-71, mobilenet.py:32-33, mobile_vit.py:20-21)
+// Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
+// Errors are TORCH_CHECK -> RuntimeError, as F.conv2d raises for bad arguments.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <array>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "po2q.h"
+
+namespace {
+
+std::string last_error() {
+    const char* e = po2q_last_error();
+    return e ? std::string(e) : std::string("po2q: unknown error");
+}
+
+void check_hip_f32(const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda(), "po2q: ", what, " must be a HIP device tensor (got ", t.device(),
+                "); the po2q ops have no CPU path");
+    TORCH_CHECK(t.scalar_type() == at::kFloat, "po2q: ", what, " must be float32 (got ", t.scalar_type(), ")");
+}
+
+// PyTorch-ROCm reports HIP devices as device type "cuda" (masquerading): the guard and
+// stream helpers of that scheme map them onto the HIP runtime
+using DeviceGuard = at::hip::HIPGuardMasqueradingAsCUDA;
+
+void* stream_of(const at::Tensor& t) {
+    return reinterpret_cast<void*>(at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream());
+}
+
+// ---- conv problem -> plan handle cache (process-wide, thread-safe) -----------------
+using Key = std::array<int64_t, 20>;  // 14 geometry + bits, fsr, mode, precision, plan index, device
+
+struct PlanEntry {
+    po2q_conv_plan* plan = nullptr;
+    size_t ws = 0;
+    bool tuned = false;  // created after po2q_qconv2d_autotune measured this problem
+    ~PlanEntry() { po2q_qconv2d_plan_destroy(plan); }
+};
+
+std::mutex g_mu;
+std::map<Key, std::unique_ptr<PlanEntry>> g_plans;
+std::vector<std::unique_ptr<PlanEntry>> g_retired;  // replaced by a tuned entry; kept alive
+
+struct Geometry {
+    std::array<int64_t, 14> g;  // N C H W K R S sh sw ph pw dh dw groups
+    std::vector<int64_t> yshape;
+};
+
+int64_t pick(at::IntArrayRef v, int i, const char* what) {
+    TORCH_CHECK(v.size() == 1 || v.size() == 2, "po2q: ", what, " must have 1 or 2 elements");
+    return v.size() == 1 ? v[0] : v[i];
+}
+
+Geometry conv_geometry(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                       at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups) {
+    check_hip_f32(x, "input");
+    check_hip_f32(w, "weight");
+    TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "po2q: expected 4-D input and weight, got ", x.dim(), "-D and ",
+                w.dim(), "-D");
+    TORCH_CHECK(x.device() == w.device(), "po2q: input and weight must be on the same device");
+    if (bias.has_value()) {
+        check_hip_f32(*bias, "bias");
+        TORCH_CHECK(bias->device() == x.device(), "po2q: bias must be on the input's device");
+        TORCH_CHECK(bias->numel() == w.size(0), "po2q: bias must have ", w.size(0), " elements");
+    }
+    TORCH_CHECK(groups > 0, "po2q: non-positive groups is not supported");
+    TORCH_CHECK(w.size(1) * groups == x.size(1), "po2q: Given groups=", groups, ", weight of size ", w.sizes(),
+                ", expected input", x.sizes(), " to have ", w.size(1) * groups, " channels, but got ", x.size(1),
+                " channels instead");
+    Geometry G;
+    const int64_t sh = pick(stride, 0, "stride"), sw = pick(stride, 1, "stride");
+    const int64_t ph = pick(padding, 0, "padding"), pw = pick(padding, 1, "padding");
+    const int64_t dh = pick(dilation, 0, "dilation"), dw = pick(dilation, 1, "dilation");
+    G.g = {x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(2), w.size(3), sh, sw, ph, pw, dh, dw, groups};
+    const int64_t P = (x.size(2) + 2 * ph - dh * (w.size(2) - 1) - 1) / sh + 1;
+    const int64_t Q = (x.size(3) + 2 * pw - dw * (w.size(3) - 1) - 1) / sw + 1;
+    G.yshape = {x.size(0), w.size(0), std::max<int64_t>(P, 0), std::max<int64_t>(Q, 0)};
+    return G;
+}
+
+// The plan for this problem: candidate `plan` (>= 0), or the tuned / heuristic plan
+// (-1); autotune != 0 measures every candidate once first (an untimed first call, as
+// torch.backends.cudnn.benchmark does), writing y.
+PlanEntry* plan_for(const Geometry& G, int64_t bits, int64_t fsr, int64_t mode, int64_t prec, int64_t plan,
+                    bool autotune, const at::Tensor& x, const at::Tensor& w, const float* bias, at::Tensor& y,
+                    bool& y_written) {
+    Key k;
+    for (int i = 0; i < 14; ++i) k[i] = G.g[i];
+    k[14] = bits; k[15] = fsr; k[16] = mode; k[17] = prec; k[18] = plan; k[19] = x.device().index();
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_plans.find(k);
+    if (it != g_plans.end() && (it->second->tuned || !autotune || plan >= 0)) return it->second.get();
+    const auto& g = G.g;
+    if (autotune && plan < 0) {
+        const size_t wsb = po2q_qconv2d_workspace_bytes(g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9],
+                                                        g[10], g[11], g[12], g[13], (int)bits, (int)fsr, (int)mode,
+                                                        (int)prec);
+        TORCH_CHECK(wsb > 0, last_error());
+        at::Tensor ws = at::empty({(int64_t)wsb}, x.options().dtype(at::kByte));
+        char desc[512];
+        const int st = po2q_qconv2d_autotune(x.data_ptr<float>(), w.data_ptr<float>(), bias, y.data_ptr<float>(),
+                                             g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11],
+                                             g[12], g[13], (int)bits, (int)fsr, (int)mode, (int)prec, ws.data_ptr(),
+                                             wsb, stream_of(x), desc, sizeof desc);
+        TORCH_CHECK(st == 0, last_error());
+        y_written = true;
+    }
+    auto e = std::make_unique<PlanEntry>();
+    const int st = po2q_qconv2d_plan_create(&e->plan, (int)plan, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8],
+                                            g[9], g[10], g[11], g[12], g[13], (int)bits, (int)fsr, (int)mode, (int)prec);
+    TORCH_CHECK(st == 0, last_error());
+    e->ws = po2q_qconv2d_plan_workspace_bytes(e->plan);
+    e->tuned = autotune && plan < 0;
+    PlanEntry* out = e.get();
+    if (it != g_plans.end()) g_retired.push_back(std::move(it->second));
+    g_plans[k] = std::move(e);
+    return out;
+}
+
+const float* opt_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+
+at::Tensor qconv2d_impl(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias_,
+                        at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
+                        int64_t bits, int64_t mode, int64_t fsr, int64_t prec, int64_t plan, int64_t autotune,
+                        const c10::optional<at::Tensor>& post_scale_, const c10::optional<at::Tensor>& post_shift_,
+                        const c10::optional<at::Tensor>& residual_, int64_t act) {
+    const Geometry G = conv_geometry(x_, w_, bias_, stride, padding, dilation, groups);
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous(), w = w_.contiguous();
+    c10::optional<at::Tensor> bias, ps, pb, res;
+    if (bias_.has_value()) bias = bias_->contiguous();
+    for (auto [src, dst, what] : {std::make_tuple(&post_scale_, &ps, "post_scale"),
+                                  std::make_tuple(&post_shift_, &pb, "post_shift")}) {
+        if (src->has_value()) {
+            check_hip_f32(**src, what);
+            TORCH_CHECK((*src)->device() == x.device(), "po2q: ", what, " must be on the input's device");
+            TORCH_CHECK((*src)->numel() == G.yshape[1], "po2q: ", what, " must have ", G.yshape[1], " elements, got ",
+                        (*src)->numel());
+            *dst = (*src)->contiguous();
+        }
+    }
+    if (residual_.has_value()) {
+        check_hip_f32(*residual_, "residual");
+        TORCH_CHECK(residual_->device() == x.device(), "po2q: residual must be on the input's device");
+        TORCH_CHECK(residual_->sizes() == at::IntArrayRef(G.yshape), "po2q: residual shape ", residual_->sizes(),
+                    " does not match the output ", at::IntArrayRef(G.yshape));
+        res = residual_->contiguous();
+    }
+    at::Tensor y = at::empty(G.yshape, x.options());
+    if (G.yshape[0] == 0) return y;  // an empty batch: torch's F.conv2d returns an empty output
+    const bool epi = ps.has_value() || pb.has_value() || res.has_value() || act != 0;
+    bool y_written = false;
+    // autotuning writes y through the plain conv; with an epilogue the tuned plan runs again
+    PlanEntry* e = plan_for(G, bits, fsr, mode, prec, plan, autotune != 0, x, w, opt_ptr(bias), y, y_written);
+    if (y_written && !epi) return y;
+    at::Tensor ws = at::empty({(int64_t)e->ws}, x.options().dtype(at::kByte));
+    const int st = po2q_qconv2d_plan_run(e->plan, x.data_ptr<float>(), w.data_ptr<float>(), opt_ptr(bias),
+                                         y.data_ptr<float>(), opt_ptr(ps), opt_ptr(pb), opt_ptr(res), (int)act,
+                                         ws.data_ptr(), e->ws, stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return y;
+}
+
+at::Tensor qconv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                   at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
+                   int64_t bits, int64_t mode, int64_t fsr, int64_t prec, int64_t plan, int64_t autotune) {
+    return qconv2d_impl(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, autotune,
+                        c10::nullopt, c10::nullopt, c10::nullopt, 0);
+}
+
+at::Tensor qconv2d_fused(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                         at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
+                         int64_t bits, int64_t mode, int64_t fsr, int64_t prec, int64_t plan, int64_t autotune,
+                         const c10::optional<at::Tensor>& post_scale, const c10::optional<at::Tensor>& post_shift,
+                         const c10::optional<at::Tensor>& residual, int64_t act) {
+    TORCH_CHECK(act >= 0 && act <= 3, "po2q: unknown activation ", act);
+    return qconv2d_impl(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, autotune,
+                        post_scale, post_shift, residual, act);
+}
+
+at::Tensor quantize(const at::Tensor& w_, int64_t bits, int64_t mode, int64_t fsr) {
+    check_hip_f32(w_, "input");
+    TORCH_CHECK(mode == 1 || mode == 2, "po2q: quantize() needs mode po2 (1) or po2+ (2)");
+    const DeviceGuard guard(w_.device());
+    const at::Tensor w = w_.contiguous();
+    at::Tensor out = at::empty_like(w);
+    const int64_t n = w.numel();
+    at::Tensor ws = at::empty({(int64_t)std::max<size_t>(po2q_quantize_workspace_bytes(n), 256)},
+                              w.options().dtype(at::kByte));
+    const int st = po2q_quantize_f32(w.data_ptr<float>(), out.data_ptr<float>(), n, (int)bits, (int)fsr, (int)mode,
+                                     ws.data_ptr(), ws.numel(), stream_of(w));
+    TORCH_CHECK(st == 0, last_error());
+    return out;
+}
+
+at::Tensor quantize_lin(const at::Tensor& w_, int64_t bits, int64_t num_iters, int64_t plus) {
+    check_hip_f32(w_, "input");
+    // the reference reduces dims 3, 2, 0 explicitly (torch.max(..., dim=3) ...)
+    TORCH_CHECK(w_.dim() == 4, "po2q: the lin quantizers need a 4-D weight (got ", w_.dim(), " dims)");
+    const DeviceGuard guard(w_.device());
+    const at::Tensor w = w_.contiguous();
+    at::Tensor out = at::empty_like(w);
+    const int st = po2q_quantize_lin_f32(w.data_ptr<float>(), out.data_ptr<float>(), w.size(0), w.size(1), w.size(2),
+                                         w.size(3), (int)bits, (int)num_iters, plus ? 1 : 0, stream_of(w));
+    TORCH_CHECK(st == 0, last_error());
+    return out;
+}
+
+// ---- Meta (shape-only) implementations ------------------------------------------
+at::Tensor qconv2d_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                        at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
+                        int64_t, int64_t, int64_t, int64_t, int64_t, int64_t) {
+    TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "po2q: expected 4-D input and weight");
+    const int64_t P = (x.size(2) + 2 * pick(padding, 0, "padding") - pick(dilation, 0, "dilation") * (w.size(2) - 1) -
+                       1) / pick(stride, 0, "stride") + 1;
+    const int64_t Q = (x.size(3) + 2 * pick(padding, 1, "padding") - pick(dilation, 1, "dilation") * (w.size(3) - 1) -
+                       1) / pick(stride, 1, "stride") + 1;
+    return at::empty({x.size(0), w.size(0), std::max<int64_t>(P, 0), std::max<int64_t>(Q, 0)}, x.options());
+}
+
+at::Tensor qconv2d_fused_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                              at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
+                              int64_t bits, int64_t mode, int64_t fsr, int64_t prec, int64_t plan, int64_t autotune,
+                              const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
+                              const c10::optional<at::Tensor>&, int64_t) {
+    return qconv2d_meta(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, autotune);
+}
+
+at::Tensor same_meta(const at::Tensor& w, int64_t, int64_t, int64_t) { return at::empty_like(w); }
+
+}  // namespace
+
+TORCH_LIBRARY(po2q, m) {
+    m.def("quantize(Tensor w, int bits, int mode, int fsr=1) -> Tensor");
+    m.def("quantize_lin(Tensor w, int bits, int num_iters=10, int plus=0) -> Tensor");
+    m.def("qconv2d(Tensor x, Tensor w, Tensor? bias, int[2] stride, int[2] padding, int[2] dilation, int groups, "
+          "int bits, int mode, int fsr=1, int precision=0, int plan=-1, int autotune=0) -> Tensor");
+    m.def("qconv2d_fused(Tensor x, Tensor w, Tensor? bias, int[2] stride, int[2] padding, int[2] dilation, "
+          "int groups, int bits, int mode, int fsr=1, int precision=0, int plan=-1, int autotune=0, "
+          "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
+    m.impl("quantize", &quantize);
+    m.impl("quantize_lin", &quantize_lin);
+    m.impl("qconv2d", &qconv2d);
+    m.impl("qconv2d_fused", &qconv2d_fused);
+}
+
+TORCH_LIBRARY_IMPL(po2q, Meta, m) {
+    m.impl("quantize", &same_meta);
+    m.impl("quantize_lin", &same_meta);
+    m.impl("qconv2d", &qconv2d_meta);
+    m.impl("qconv2d_fused", &qconv2d_fused_meta);
+}

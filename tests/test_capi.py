@@ -84,17 +84,19 @@ def test_workspace_sizes_are_small(shape):
         assert 0 < nbytes < 64 * K * max(Cg, 4) * R * S + 65536
 
 
-def test_cpu_tensors_raise_no_fallback():
+def test_cpu_conv_raises_quantizer_restated():
+    """The conv has no CPU path (raises); the PO2 quantizers take CPU tensors through the
+    product-side torch restatement, never through the oracle."""
     import torch
 
     from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
     from po2_quantization_amd.utils.quantizers import PowerOfTwoQuantizer, quantizer_dict
 
     w = torch.randn(4, 4, 3, 3)
-    with pytest.raises(RuntimeError, match="HIP device"):
-        PowerOfTwoQuantizer.apply(w, 4)
-    with pytest.raises(RuntimeError, match="HIP device"):
-        quantizer_dict["po2+"].forward(None, w, bits=3)
+    y = PowerOfTwoQuantizer.apply(w, 4)
+    assert y.dtype == w.dtype and y.device == w.device
+    assert torch.equal(y, _lib.restated_quantize(w, 4, "po2"))
+    assert torch.equal(quantizer_dict["po2+"].forward(None, w, bits=3), _lib.restated_quantize(w, 3, "po2+"))
     conv = QuantizedConv2d(4, 4, 3, quantize_fn=PowerOfTwoQuantizer, bits=4)
     with pytest.raises(RuntimeError, match="HIP device"):
         conv(torch.randn(1, 4, 8, 8))

@@ -81,11 +81,42 @@ def test_straight_through_backward():
     assert torch.equal(w.grad, g)
 
 
-def test_empty_and_wrong_dtype_raise():
+def test_empty_raises():
     with pytest.raises(RuntimeError, match="numel"):
         PowerOfTwoQuantizer.apply(torch.empty(0, device=DEV), 4)
-    with pytest.raises(RuntimeError, match="float32"):
-        PowerOfTwoQuantizer.apply(torch.randn(8, device=DEV, dtype=torch.float64), 4)
+    with pytest.raises(RuntimeError, match="numel"):
+        PowerOfTwoQuantizer.apply(torch.empty(0, device=DEV, dtype=torch.float64), 4)
+
+
+def test_fp64_bf16_on_gpu_keep_dtype_match_reference():
+    """Non-fp32 HIP tensors take the product-side torch restatement: dtype
+    and device preserved.  Against the reference's CPU outputs (tests/golden/
+    quant_kat_dtypes.npz): equal except where the device's log2 lands on the other side of
+    a rounding tie than the CPU's (the reference's own formula run on this GPU decides those
+    the same way) -- and there only by one exponent step."""
+    from po2_quantization_amd.utils.quantizers import PowerOfTwoPlusQuantizer
+    from tests.test_restated_quantizer import _load, dtype_items
+
+    n = total = off = 0
+    for d, key, dt, name, mode, bits in dtype_items():
+        x = _load(d["x/%s/%s" % (dt, name)], dt).to(DEV)
+        want = _load(d[key], dt).double()
+        Q = PowerOfTwoQuantizer if mode == "po2" else PowerOfTwoPlusQuantizer
+        y = Q.apply(x, bits)
+        assert y.dtype == x.dtype and y.device == x.device
+        y = y.cpu().double()
+        nan = torch.isnan(y)
+        assert torch.equal(nan, torch.isnan(want)), key
+        diff = y[~nan] != want[~nan]
+        if diff.any():
+            ratio = (y[~nan][diff] / want[~nan][diff]).abs()
+            assert bool(((ratio == 2.0) | (ratio == 0.5)).all()), key
+        total += int((~nan).sum())
+        off += int(diff.sum())
+        n += 1
+    assert n == 48
+    assert off <= 0.005 * total, (off, total)
+    # CPU tensors of the same dtypes: the reference's outputs bit for bit (CPU test suite)
 
 
 def test_stream_semantics_no_host_sync():

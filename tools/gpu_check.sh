@@ -38,6 +38,9 @@ for s in $STEPS; do
                fi ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
+        layers32) run layers32 600 python tools/layer_bench.py --image 32 --tune --torch ;;
+        bench32) run bench32 600 python bench.py --image 32 --steps 20 --warmup 3 --no-cpu-baseline ;;
+        bench32g) run bench32g 600 python bench.py --image 32 --steps 50 --warmup 3 --graph --no-cpu-baseline ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep0) run sweep0 600 python tools/tile_sweep.py --shapes 0 --iters 21 ;;
