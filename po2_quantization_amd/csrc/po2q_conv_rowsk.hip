@@ -366,13 +366,17 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                     af[pl][grp] = __builtin_bit_cast(
                         bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
 #pragma unroll
-            for (int rr = 0; rr < 3; ++rr)
+            for (int rr = 0; rr < 3; ++rr) {
+                // tap row rr of halo row j lands on segment output row j - rr: skip the
+                // MFMAs of the edge rows whose output lies outside the segment (wave-uniform)
+                if (j - rr < 0 || j - rr >= rbe) continue;
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                     for (int grp = 0; grp < NGW; ++grp)
                         acc[SL[rr]][grp] =
                             __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr][ks], acc[SL[rr]][grp], 0, 0, 0);
+            }
         }
         // output halo-index j-1 (row p0 + j - 2) is complete
         constexpr int D = (S + 2) % 3;

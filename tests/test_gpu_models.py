@@ -64,3 +64,34 @@ def test_state_dict_keys_match_reference():
     for mt in ("resnet20", "resnet56", "mobilenet", "mobilevit"):
         m = get_model(mt, 10, None, 4, (32, 32))
         assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == keys[mt]
+
+
+@pytest.mark.parametrize("spec,q,bits", [("resnet56", "po2", 4), ("resnet20", "po2+", 3), ("mobilenet", "po2+", 4),
+                                         ("mobilenet", "po2", 2), ("mobilevit", "po2+", 2), ("mobilevit", "po2", 4)])
+def test_model_quantization_error_through_hip_quantizer(spec, q, bits):
+    """get_quantization_error (models/quantized_conv.py:40-45, model-level sums with the
+    reference's counting quirks) through the HIP quantizer == the reference's values."""
+    d = load_npz("models.npz")
+    m = build(spec, q, bits)
+    e, n = m.get_quantization_error()
+    ref_e, ref_n = d["qerr/%s/%s/%d" % (spec, q, bits)]
+    assert int(n) == int(ref_n)
+    assert abs(float(torch.as_tensor(e).detach().cpu()) - ref_e) <= 1e-5 * ref_e
+
+
+def test_layer_quantization_error_vs_oracle():
+    """QuantizedConv2d.get_quantization_error on GPU: (sum (Q(w) - w)^2, numel), Q bit-exact."""
+    from oracle import oracle as O
+    from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
+
+    g = torch.Generator().manual_seed(5)
+    for qn in ("po2", "po2+"):
+        conv = QuantizedConv2d(32, 64, 3, quantize_fn=quantizer_dict[qn], bits=4)
+        with torch.no_grad():
+            conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.05)
+        conv = conv.to(DEV)
+        e, n = conv.get_quantization_error()
+        w = conv.weight.detach().cpu().numpy()
+        ref = O.sq_error(w, O.quantize(w, 4, qn))
+        assert int(n) == w.size
+        assert abs(float(torch.as_tensor(e).detach().cpu()) - ref) <= 1e-5 * ref  # fp32 sum (torch) vs fp64

@@ -45,7 +45,10 @@ for s in $STEPS; do
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep0) run sweep0 600 python tools/tile_sweep.py --shapes 0 --iters 21 ;;
         sweep3) run sweep3 600 python tools/tile_sweep.py --shapes 3 --iters 21 ;;
+        sweep6) run sweep6 600 python tools/tile_sweep.py --shapes 6 --iters 21 ;;
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
+        pmcs3) run pmcs3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" s3 "conv_rowsk" all
+               python3 tools/pmc_summary.py gpurun_out/pmc_s3 > gpurun_out/pmc_s3_summary.txt 2>&1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
         copyprobe) run copyprobe 300 tools/copy_probe 20 ;;
         ringprobe) run ringprobe 300 tools/copy_probe 20 1 ;;
