@@ -213,6 +213,26 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
  * Handles are immutable after creation; run may be called concurrently on one handle.
  * Replaces per call: QuantizedConv2d.forward (models/quantized_conv.py:32-38).
  */
+/*
+ * QAT backward, weight gradient: the gradient autograd takes through
+ * F.conv2d(x, Q(w), ...) for w -- the straight-through estimator passes it unchanged
+ * (utils/quantizers.py:34-36; train.py:79-91 runs loss.backward()):
+ *   dw[k][c][r][s] = sum_{n,p,q} dy[n][k][p][q] * x[n][c][p*sh + r*dil_h - pad_h][q*sw + s*dil_w - pad_w]
+ * fp32 MFMA (exact products, fp32 accumulation, a fixed summation order: deterministic).
+ * groups == 1, R x S in {1x1, 3x3}; PO2Q_ERR_UNSUPPORTED otherwise (the caller falls back).
+ * The input gradient needs no entry of its own: for stride 1 it is po2q_qconv2d_f32 of dy
+ * with the weight transposed (K <-> C) and flipped, padding R - 1 - pad (Q is
+ * permutation-equivariant, so the same PO2 weights result).
+ */
+size_t po2q_qconv2d_wgrad_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
+                                          int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
+                                          int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups);
+int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw,
+                           int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                           int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
+                           int64_t dil_h, int64_t dil_w, int64_t groups,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
 typedef struct po2q_conv_plan po2q_conv_plan;
 int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index,
                              int64_t N, int64_t C, int64_t H, int64_t W,

@@ -49,6 +49,8 @@ EXPORTS = (
     "po2q_qconv2d_plan_run",
     "po2q_qconv2d_plan_describe",
     "po2q_qconv2d_plan_destroy",
+    "po2q_qconv2d_wgrad_workspace_bytes",
+    "po2q_qconv2d_wgrad_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -408,6 +410,24 @@ class SplitConv:
         _check(load().po2q_qconv2d_packed_f32(self._plan(), xc.data_ptr(), bp, y.data_ptr(), *self.key,
                                               self.ws.data_ptr(), self.ws.numel(), _stream(xc.device)))
         return y
+
+
+def conv_wgrad(x, gy, wshape, stride=1, padding=0, dilation=1, groups=1):
+    """QAT backward, weight gradient of conv2d(x, w) for grad_output gy (native fp32 MFMA
+    kernel, po2q_qconv2d_wgrad_f32); groups == 1 and a 1x1 / 3x3 kernel."""
+    _require_hip_f32(x, "input")
+    _require_hip_f32(gy, "grad_output")
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    dh, dw = _pair(dilation)
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: conv_wgrad needs the operator library (PO2Q_LIB selects another build)")
+    return _op_call(O.conv_wgrad, x, gy, list(wshape), [sh, sw], [ph, pw], [dh, dw], int(groups))
+
+
+def wgrad_supported(wshape, groups):
+    return int(groups) == 1 and tuple(wshape[2:]) in ((1, 1), (3, 3))
 
 
 def _plan_choice(key, plan):

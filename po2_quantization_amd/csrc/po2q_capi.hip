@@ -335,6 +335,14 @@ int po2q_qconv2d_autotune(const float* x, const float* w, const float* bias, flo
     }
     for (int i = 0; i < (int)cands.size(); ++i)
         if (best < 0 || tmin[i] < tmin[best]) best = i;
+    // within 1 % (timing noise), prefer a plan with fused weight staging: one launch per
+    // layer instead of pack + conv (fewer kernel boundaries in a real chain)
+    if (best >= 0 && !cands[best].fp) {
+        int bf = -1;
+        for (int i = 0; i < (int)cands.size(); ++i)
+            if (cands[i].fp && tmin[i] <= 1.01f * tmin[best] && (bf < 0 || tmin[i] < tmin[bf])) bf = i;
+        if (bf >= 0) best = bf;
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (st) return st;

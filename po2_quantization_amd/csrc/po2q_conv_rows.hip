@@ -373,7 +373,7 @@ static int cdivr(int a, int b) { return (a + b - 1) / b; }
 void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
 hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
-                             int act, bool epi);
+                             int act, bool epi, const WQuant& q);
 // full-row blocks (po2q_conv_rowsf.hip: C = K = 16, plan vrx = 4)
 void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
 hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
@@ -498,8 +498,8 @@ static hipError_t rows_dispatch(const ConvPlan& p, const float* x, const uint16_
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                    const float* bias, float* y, hipStream_t s, const WQuant& q) {
     if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false, q);
-    if (p.fp) return hipErrorInvalidValue;  // fused weight staging: full-row plans only
-    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false);
+    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false, q);
+    if (p.fp) return hipErrorInvalidValue;  // fused weight staging: full-row / C = 64 plans only
 #ifdef PO2Q_ROWS_DIAG
     const char* dbg = getenv("PO2Q_ROWS_DEBUG");  // timing ablation (outputs are wrong)
     if (dbg && p.CC == 32 && p.NT == 2) {
@@ -537,8 +537,8 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s, const WQuant& q) {
     if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, ps, pb, act, true, q);
+    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true, q);
     if (p.fp) return hipErrorInvalidValue;
-    if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true);
     return rows_dispatch<true>(p, x, packed, scale, bias, y, s, ps, pb, act);
 }
 

@@ -32,6 +32,7 @@
 
 #include "po2q_epi.h"
 #include "po2q_internal.h"
+#include "po2q_quant_dev.h"
 #include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
 
@@ -69,6 +70,7 @@ struct RowsKArgs {
     const float* pb;
     int act;
     const float* res;  // RES: y = act(y * ps + pb + res), res [N, K, P, Q] (loader wave DMAs it)
+    WQuant q;          // FP: raw weights + quantizer parameters
 };
 
 // The LW loader wave: every DMA of the block, the layout the MFMA waves' own DMAs
@@ -157,7 +159,10 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 // the non-temporal policy
 // RES (with LW, TT, EPI): the residual add inside the kernel (the loader wave DMAs the
 //     residual rows next to the output tile; act after the add)
-template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, int NTS = 0, bool RES = false>
+// FP (plan field fp, not with LW): the block reduces max|w| and each wave quantizes +
+//     packs its own VGPR-resident B fragments (po2q_quant_dev.h wq_*): one launch per layer
+template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, int NTS = 0, bool RES = false,
+          bool FP = false>
 __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -203,17 +208,34 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
     }
 
     // ---- this wave's weights: B[r][ks = chunk*3 + s] for output channels 16w..16w+15
+    static_assert(!(FP && LW), "the loader wave keeps its own barrier count");
     bf16x8 bw[3][KSC];
+    float scale;
+    if constexpr (FP) {
+        // scratch in the raw ring, free until the first DMA below
+        unsigned* red = reinterpret_cast<unsigned*>(raw);
+        unsigned* thr = red + 16;
+        bool fin;
+        scale = wq_prologue(a.q, thr, red, 4, fin);
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int ks = 0; ks < KSC; ++ks)
-            bw[r][ks] = __builtin_bit_cast(bf16x8, wpk[((r * KSC + ks) * WN + wn) * 64 + lane]);
+            for (int ks = 0; ks < KSC; ++ks)
+                bw[r][ks] = __builtin_bit_cast(
+                    bf16x8, wq_frag_rows(a.q, C, C, 32, WN, KSC, ((r * KSC + ks) * WN + wn) * 64 + lane, scale, fin, thr));
+        __syncthreads();  // every threshold read done before the ring's DMAs
+    } else {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int ks = 0; ks < KSC; ++ks)
+                bw[r][ks] = __builtin_bit_cast(bf16x8, wpk[((r * KSC + ks) * WN + wn) * 64 + lane]);
+        scale = *scale_p;
+    }
     const int kout = 16 * wn + (lane & 15);
     float bk = bias ? bias[kout] : 0.0f;
     float eps_ = (EPI && a.ps) ? a.ps[kout] : 1.0f;
     float epb_ = (EPI && a.pb) ? a.pb[kout] : 0.0f;
-    const float scale = *scale_p;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -521,6 +543,12 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 const int64_t items = (int64_t)p.N * d.tilesP * d.tilesQ;
                 d.blocks = (items + 7) / 8 * 8;
                 out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0) + (vrx == vrxs[0] ? 0.0 : 0.02), d});
+                // C = 64 direct stores with fused weight staging (one launch per layer)
+                if (b.C == 64 && vrx == 1) {
+                    ConvPlan f = d;
+                    f.fp = 1;
+                    out.push_back({0.899 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), f});
+                }
                 // the default variants (C = 64 direct stores, C = 32 loader wave) also with
                 // non-temporal output stores (nts 1), non-temporal x loads (2) or both (3)
                 if ((b.C == 64 && vrx == 1) || (b.C == 32 && vrx == 3))
@@ -534,7 +562,7 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
 
 hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                              const float* bias, float* y, hipStream_t s, const float* ps, const float* pb,
-                             int act, bool epi) {
+                             int act, bool epi, const WQuant& q) {
     RowsKArgs a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.nstrip = p.tilesQ;
@@ -544,6 +572,19 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     a.pb = pb;
     a.act = act;
     a.res = nullptr;
+    a.q = q;
+    if (p.fp) {  // fused weight staging: C = 64 direct-store plans
+        if (!q.w || p.vrx != 1 || p.C != 64 || p.nts) return hipErrorInvalidValue;
+#define PO2Q_RKF(d, e)                                                                                     \
+    if (p.pd == d && epi == e) {                                                                             \
+        hipLaunchKernelGGL((conv_rowsk<64, d, false, false, e, 0, 0, false, true>), dim3((unsigned)p.blocks), \
+                           dim3(kThreads), p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a); \
+        return hipGetLastError();                                                                            \
+    }
+        PO2Q_RKF(3, false) PO2Q_RKF(2, false) PO2Q_RKF(3, true) PO2Q_RKF(2, true)
+#undef PO2Q_RKF
+        return hipErrorInvalidValue;
+    }
 #define PO2Q_RK1(c, d, e, v, tt, lw)                                                                      \
     if (p.C == c && p.pd == d && epi == e && p.vrx == v && !p.nts) {                                         \
         hipLaunchKernelGGL((conv_rowsk<c, d, tt, lw, e>), dim3((unsigned)p.blocks), dim3(kThreads + (lw ? 64 : 0)), \

@@ -10,6 +10,8 @@
 //                        (models/quantized_conv.py:32-38)
 //   po2q::qconv2d_fused  the same + eval BatchNorm affine, residual add and activation of
 //                        the blocks (resnet.py:55-71, mobilenet.py:32-33, mobile_vit.py:20-21)
+//   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
+//                        STE, utils/quantizers.py:34-36)
 // Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
 // Errors are TORCH_CHECK -> RuntimeError, as F.conv2d raises for bad arguments.
 #include <ATen/ATen.h>
@@ -227,6 +229,30 @@ at::Tensor quantize_lin(const at::Tensor& w_, int64_t bits, int64_t num_iters, i
     return out;
 }
 
+// QAT backward: weight gradient (fp32 MFMA; see po2q_qconv2d_wgrad_f32)
+at::Tensor conv_wgrad(const at::Tensor& x_, const at::Tensor& dy_, at::IntArrayRef wshape, at::IntArrayRef stride,
+                      at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups) {
+    check_hip_f32(x_, "input");
+    check_hip_f32(dy_, "grad_output");
+    TORCH_CHECK(x_.dim() == 4 && dy_.dim() == 4 && wshape.size() == 4, "po2q: wgrad: 4-D input, grad_output, weight");
+    TORCH_CHECK(x_.device() == dy_.device(), "po2q: wgrad: input and grad_output on different devices");
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous(), dy = dy_.contiguous();
+    const int64_t sh = pick(stride, 0, "stride"), sw = pick(stride, 1, "stride");
+    const int64_t ph = pick(padding, 0, "padding"), pw = pick(padding, 1, "padding");
+    const int64_t dh = pick(dilation, 0, "dilation"), dw = pick(dilation, 1, "dilation");
+    const size_t wsb = po2q_qconv2d_wgrad_workspace_bytes(x.size(0), x.size(1), x.size(2), x.size(3), wshape[0],
+                                                          wshape[2], wshape[3], sh, sw, ph, pw, dh, dw, groups);
+    TORCH_CHECK(wsb > 0, last_error());
+    at::Tensor ws = at::empty({(int64_t)wsb}, x.options().dtype(at::kByte));
+    at::Tensor gw = at::empty(wshape, x.options());
+    const int st = po2q_qconv2d_wgrad_f32(x.data_ptr<float>(), dy.data_ptr<float>(), gw.data_ptr<float>(), x.size(0),
+                                          x.size(1), x.size(2), x.size(3), wshape[0], wshape[2], wshape[3], sh, sw, ph,
+                                          pw, dh, dw, groups, ws.data_ptr(), wsb, stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return gw;
+}
+
 // ---- Meta (shape-only) implementations ------------------------------------------
 at::Tensor qconv2d_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                         at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
@@ -249,6 +275,11 @@ at::Tensor qconv2d_fused_meta(const at::Tensor& x, const at::Tensor& w, const c1
 
 at::Tensor same_meta(const at::Tensor& w, int64_t, int64_t, int64_t) { return at::empty_like(w); }
 
+at::Tensor conv_wgrad_meta(const at::Tensor& x, const at::Tensor&, at::IntArrayRef wshape, at::IntArrayRef,
+                           at::IntArrayRef, at::IntArrayRef, int64_t) {
+    return at::empty(wshape, x.options());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(po2q, m) {
@@ -259,6 +290,8 @@ TORCH_LIBRARY(po2q, m) {
     m.def("qconv2d_fused(Tensor x, Tensor w, Tensor? bias, int[2] stride, int[2] padding, int[2] dilation, "
           "int groups, int bits, int mode, int fsr=1, int precision=0, int plan=-1, int autotune=0, "
           "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
+    m.def("conv_wgrad(Tensor x, Tensor dy, int[] wshape, int[2] stride, int[2] padding, int[2] dilation, "
+          "int groups=1) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
@@ -266,6 +299,7 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("quantize_lin", &quantize_lin);
     m.impl("qconv2d", &qconv2d);
     m.impl("qconv2d_fused", &qconv2d_fused);
+    m.impl("conv_wgrad", &conv_wgrad);
 }
 
 TORCH_LIBRARY_IMPL(po2q, Meta, m) {
@@ -273,4 +307,5 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("quantize_lin", &same_meta);
     m.impl("qconv2d", &qconv2d_meta);
     m.impl("qconv2d_fused", &qconv2d_fused_meta);
+    m.impl("conv_wgrad", &conv_wgrad_meta);
 }

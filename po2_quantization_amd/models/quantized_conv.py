@@ -12,7 +12,9 @@ same get_quantization_error().  forward() runs the fused libpo2q path:
       -> qw = quantize_fn.apply(weight, bits), then the native conv of qw
 
 Backward (QAT) keeps the reference's semantics: straight-through estimator on
-the weight (quantizers.py:34-36), conv gradients of the quantized weight.
+the weight (quantizers.py:34-36), conv gradients of the quantized weight -- the input
+gradient of stride-1 layers through the native bf16x3 conv kernels, the weight gradient
+through the native fp32-MFMA wgrad kernel (_QConv2dFn.backward).
 Inputs must be fp32 HIP tensors; there is no CPU path.
 
 Inference fusion: `fused(x, bn=, act=, residual=)` runs the conv
@@ -35,19 +37,47 @@ class _QConv2dFn(torch.autograd.Function):
         y = _lib.qconv2d(x, weight, bias, stride, padding, dilation, groups, bits, mode, 1, precision)
         ctx.save_for_backward(x, weight, bias)
         ctx.conf = (stride, padding, dilation, groups, bits, mode)
+        ctx.precision = precision
         return y
 
     @staticmethod
     def backward(ctx, gy):
+        """The gradients autograd takes through F.conv2d(x, Q(w), bias) with the straight-
+        through estimator on Q (quantizers.py:34-36; train.py:79-91), natively where the
+        kernels cover the layer:
+          input  -- stride 1, dilation 1, groups 1: the fused quantize + conv of gy with the
+                    weight transposed (K <-> C) and flipped, padding R-1-p: Q commutes with
+                    that permutation, so these are the same exact PO2 weights (bf16x3);
+          weight -- groups 1, 1x1 / 3x3: po2q_qconv2d_wgrad_f32 (fp32 MFMA);
+          bias   -- sum of gy over N, P, Q.
+        Anything else (stride-2 input gradients, grouped / depthwise layers) is issued as one
+        aten.convolution_backward of Q(w), as autograd would."""
         x, weight, bias = ctx.saved_tensors
         stride, padding, dilation, groups, bits, mode = ctx.conf
-        qw = weight if mode == "none" else _lib.quantize(weight, bits, mode)
-        # one convolution_backward for the input, weight (STE: d qw / d w = 1) and bias
-        # gradients, as autograd issues for F.conv2d(x, qw, bias)
-        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]]
-        gx, gw, gb = torch.ops.aten.convolution_backward(
-            gy, x, qw, None if bias is None else [bias.shape[0]], list(stride), list(padding), list(dilation),
-            False, [0, 0], groups, mask)
+        gy = gy.contiguous()
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        R, S = weight.shape[2], weight.shape[3]
+        pad = _lib._pair(padding)
+        native_x = (need_x and tuple(_lib._pair(stride)) == (1, 1) and tuple(_lib._pair(dilation)) == (1, 1)
+                    and groups == 1 and pad[0] <= R - 1 and pad[1] <= S - 1)
+        native_w = need_w and _lib.wgrad_supported(weight.shape, groups)
+        gx = gw = gb = None
+        if native_x:
+            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
+            gx = _lib.qconv2d(gy, wt, None, 1, (R - 1 - pad[0], S - 1 - pad[1]), 1, 1, bits, mode, 1, ctx.precision)
+        if native_w:
+            gw = _lib.conv_wgrad(x, gy, weight.shape, stride, padding, dilation, groups)
+        if need_b:
+            gb = gy.sum(dim=(0, 2, 3))
+        rest_x, rest_w = need_x and not native_x, need_w and not native_w
+        if rest_x or rest_w:
+            qw = weight if mode == "none" else _lib.quantize(weight, bits, mode)
+            rx, rw, _ = torch.ops.aten.convolution_backward(
+                gy, x, qw, None, list(stride), list(padding), list(dilation), False, [0, 0], groups,
+                [rest_x, rest_w, False])
+            gx = rx if rest_x else gx
+            gw = rw if rest_w else gw
         return gx, gw, gb, None, None, None, None, None, None, None
 
 

@@ -1,0 +1,95 @@
+"""GPU parity of the native QAT backward: the gradients autograd takes
+through F.conv2d(x, Q(w), bias) with the straight-through estimator on Q (reference
+utils/quantizers.py:34-36, train.py:79-91), against torch's own convolution_backward of
+the bit-exact Q(w) in fp64 on the CPU (a plain PyTorch reference).  Bar: normwise 1e-5."""
+import pytest
+import torch
+
+from po2_quantization_amd import _lib
+from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
+from po2_quantization_amd.utils.quantizers import quantizer_dict
+from tests._util import CONV_TOL
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def nerr(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
+
+
+def ref_grads(x, w, b, gy, qn, bits, stride, pad):
+    qw = w if qn is None else _lib.quantize(w, bits, qn)
+    gx, gw, gb = torch.ops.aten.convolution_backward(
+        gy.double().cpu(), x.double().cpu(), qw.double().cpu(), None if b is None else [b.shape[0]],
+        [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1, [True, True, b is not None])
+    return gx, gw, gb
+
+
+SHAPES = [  # N, C, H, W, K, R, stride, pad, bias, quantizer
+    (2, 16, 20, 20, 16, 3, 1, 1, False, "po2"),
+    (2, 32, 12, 12, 32, 3, 1, 1, False, "po2+"),
+    (1, 64, 10, 10, 64, 3, 1, 1, True, "po2"),
+    (2, 16, 17, 17, 32, 3, 2, 1, False, "po2"),    # stride 2: input grad via aten, weight grad native
+    (2, 16, 16, 16, 32, 1, 2, 0, False, "po2+"),   # 1x1 projection
+    (1, 8, 9, 70, 24, 3, 1, 1, True, "po2"),       # ragged channels / columns
+    (3, 16, 8, 8, 16, 3, 1, 1, False, None),       # plain conv (quantize_fn None)
+    (2, 20, 7, 5, 36, 3, 1, 2, False, "po2"),      # padding 2 (input grad padding 0)
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_qconv_backward_vs_torch_fp64(shape):
+    N, C, H, W, K, R, st, pad, bias, qn = shape
+    g = torch.Generator().manual_seed(N * 1000 + C * 10 + K)
+    conv = QuantizedConv2d(C, K, R, stride=st, padding=pad, bias=bias,
+                           quantize_fn=quantizer_dict[qn] if qn else None, bits=4)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.2)
+        if bias:
+            conv.bias.copy_(torch.randn(K, generator=g))
+    conv = conv.to(DEV)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV).requires_grad_(True)
+    y = conv(x)
+    gy = torch.randn(y.shape, generator=g).to(DEV)
+    y.backward(gy)
+    rx, rw, rb = ref_grads(x.detach(), conv.weight.detach(), conv.bias, gy, qn, 4, st, pad)
+    assert nerr(x.grad, rx) <= CONV_TOL, nerr(x.grad, rx)
+    assert nerr(conv.weight.grad, rw) <= CONV_TOL, nerr(conv.weight.grad, rw)
+    if bias:
+        assert nerr(conv.bias.grad, rb) <= CONV_TOL
+
+
+@pytest.mark.parametrize("layer", [(16, 224, 16, 3, 1, 1), (32, 112, 32, 3, 1, 1), (64, 56, 64, 3, 1, 1),
+                                   (16, 224, 32, 3, 2, 1), (32, 112, 64, 1, 2, 0)])
+def test_full_size_resnet56_backward_vs_torch(layer):
+    """ResNet56 @224 layer shapes (bs = 16): native input / weight gradients against
+    torch's fp32 GPU convolution_backward of Q(w)."""
+    C, H, K, R, st, pad = layer
+    torch.manual_seed(3)
+    x = torch.relu(torch.randn(16, C, H, H, device=DEV))
+    w = torch.randn(K, C, R, R, device=DEV) * (2.0 / (K * R * R)) ** 0.5
+    P = (H + 2 * pad - R) // st + 1
+    gy = torch.randn(16, K, P, P, device=DEV)
+    gw = _lib.conv_wgrad(x, gy, w.shape, st, pad, 1, 1)
+    qw = _lib.quantize(w, 4, "po2")
+    rx, rw, _ = torch.ops.aten.convolution_backward(gy, x, qw, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                     [True, True, False])
+    assert nerr(gw, rw) <= CONV_TOL, nerr(gw, rw)
+    if st == 1:
+        wt = w.flip(2, 3).transpose(0, 1).contiguous()
+        gx = _lib.qconv2d(gy, wt, None, 1, R - 1 - pad, 1, 1, 4, "po2")
+        assert nerr(gx, rx) <= CONV_TOL, nerr(gx, rx)
+
+
+def test_wgrad_deterministic_and_unsupported():
+    torch.manual_seed(4)
+    x = torch.randn(4, 32, 24, 24, device=DEV)
+    gy = torch.randn(4, 16, 24, 24, device=DEV)
+    a = _lib.conv_wgrad(x, gy, (16, 32, 3, 3), 1, 1)
+    b = _lib.conv_wgrad(x, gy, (16, 32, 3, 3), 1, 1)
+    assert torch.equal(a, b)  # fixed summation order, no atomics
+    assert not _lib.wgrad_supported((16, 32, 5, 5), 1) and not _lib.wgrad_supported((16, 8, 3, 3), 4)
+    with pytest.raises(_lib.Po2qError):
+        _lib.conv_wgrad(x, gy, (16, 32, 5, 5), 1, 2)

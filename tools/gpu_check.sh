@@ -37,6 +37,15 @@ for s in $STEPS; do
                    echo "stopping: conv GPU tests did not pass"; exit 1
                fi ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        models) run models_c2 300 python tools/model_bench.py --model resnet56 --image 32 --classes 10 --graph
+                run models_c3 300 python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --graph
+                run models_c5 300 python tools/model_bench.py --model mobilevit --image 256 --batch 64 --quantizer po2+ --bits 2 --graph
+                run models_c4 300 python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
+        profmb) run profmb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profmb -o run \
+                  -- python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --only-fused ;;
+        bwd) run bwd224 600 python tools/bwd_bench.py --batch 64
+             run bwd32 600 python tools/bwd_bench.py --batch 256 --image 32
+             run qatb 600 python tools/qat_bench.py resnet56 ;;
         layers) run layers 600 python tools/layer_bench.py --torch ;;
         layers32) run layers32 600 python tools/layer_bench.py --image 32 --tune --torch ;;
         bench32) run bench32 600 python bench.py --image 32 --steps 20 --warmup 3 --no-cpu-baseline ;;

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--graph", action="store_true",
+                    help="also time the fused forward replayed from a HIP graph (small images: launch-bound)")
+    ap.add_argument("--only-fused", action="store_true")
     args = ap.parse_args()
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
@@ -54,16 +57,32 @@ def main():
            "bits": args.bits}
     with torch.no_grad():
         for name, fuse in (("fused", True), ("unfused", False)):
+            if args.only_fused and not fuse:
+                continue
             quantized_conv.INFERENCE_FUSION = fuse
             t = timed(lambda: m(x), args.steps, args.warmup)
             res[name + "_ms"] = round(t * 1e3, 3)
             res[name + "_images_per_s"] = round(args.batch / t, 1)
-        quantized_conv.INFERENCE_FUSION = True
-        ya = m(x)
-        quantized_conv.INFERENCE_FUSION = False
-        yb = m(x)
-        quantized_conv.INFERENCE_FUSION = True
-    res["fused_vs_unfused_normwise"] = float((ya - yb).abs().max() / yb.abs().max())
+        if args.graph:
+            quantized_conv.INFERENCE_FUSION = True
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                m(x)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                m(x)
+            t = timed(g.replay, args.steps * 4, args.warmup)
+            res["graph_fused_ms"] = round(t * 1e3, 3)
+            res["graph_fused_images_per_s"] = round(args.batch / t, 1)
+        if not args.only_fused:
+            quantized_conv.INFERENCE_FUSION = True
+            ya = m(x)
+            quantized_conv.INFERENCE_FUSION = False
+            yb = m(x)
+            quantized_conv.INFERENCE_FUSION = True
+            res["fused_vs_unfused_normwise"] = float((ya - yb).abs().max() / yb.abs().max())
     print(json.dumps(res), flush=True)
 
 
