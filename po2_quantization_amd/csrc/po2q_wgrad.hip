@@ -22,10 +22,12 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/po2q.h"
 #include "po2q_internal.h"
+#include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
 
 namespace po2q {
@@ -142,6 +144,249 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ pa
     }
 }
 
+
+// ---- register-streaming kernel (dilation 1, equal strides 1 or 2, 1x1 / 3x3) ------------
+//
+// The reduction (n, p, q) is long and the output (K x C x R x S) small, so the kernel is
+// built around one long, resident accumulator set per wave and operands streamed straight
+// from HBM into VGPRs (no LDS staging):
+//   * wave work item = (image n, strip of 16 output columns, segment of RB output rows) of
+//     one channel group (16*KW output x 16*CW input channels); lane (ch = l & 15,
+//     pj = l >> 4) holds dy[k0 + ch][p][q' .. q'+3] (one dwordx4, q' = strip*16 + 4 pj) and
+//     the input span x[c0 + ch][h][SH*q' - pw ...] the four pixels' taps touch;
+//   * MFMA k-slot pj of v_mfma_f32_16x16x4f32 number m takes pixel q' + m, so one dwordx4
+//     of dy and one span of x feed 4 * R * S * KW * CW MFMAs; D[k][c] per tap stays in the
+//     wave's accumulators for the whole segment;
+//   * stride 1, 3x3: the three x rows of an output row are a 4-slot register ring -- each
+//     step loads one new x row and one dy row for the NEXT step (the compiler's counted
+//     vmcnt wait covers the current one); other shapes load their R rows one step ahead;
+//   * out-of-image rows / columns, channels past C / K and pixels past P / Q load as zero
+//     (out-of-range buffer offsets), so no branch in the loop depends on position;
+//   * the 4 waves of a block (4 consecutive items of one channel group) sum their tiles in
+//     LDS in a fixed order and the block writes one partial; wgrad2_reduce sums the partials
+//     of a channel group in a fixed order (deterministic, no atomics).
+struct Wgrad2Args {
+    int N, C, H, W, K, P, Q, ph, pw;
+    int RB, nseg, nstrip;  // output rows per segment, segments, 16-column strips
+    int items;             // work items per channel group: N * nseg * nstrip
+    int bpg;               // blocks per channel group: ceil(items / 4)
+    int KG, CG;            // channel groups along K (16*KW each) and C (16*CW each)
+};
+
+constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past every range: loads 0
+
+__device__ __forceinline__ float wg_ld1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+}
+__device__ __forceinline__ floatx4 wg_ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+
+template <int R, int S, int SH, int PW, int KW, int CW, bool VEC>
+__global__ __launch_bounds__(256, KW * CW == 4 ? 1 : 2) void wgrad2_f32(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     float* __restrict__ part, Wgrad2Args a) {
+    constexpr int NT = R * S;
+    constexpr int SPAN = 3 * SH + S;                           // x columns of 4 pixels' taps
+    constexpr int NB = VEC ? (SPAN - PW) / 4 : 0;              // dwordx4 pieces of the span
+    constexpr int NTAIL = VEC ? SPAN - PW - 4 * NB : 0;        // dwords after them
+    constexpr bool RING = (SH == 1 && R == 3);
+    __shared__ floatx4 red[4][NT][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = blockIdx.x / a.bpg, bi = blockIdx.x - g * a.bpg;
+    const int kg = g / a.CG, cg = g - kg * a.CG;
+    const int item = bi * 4 + wave;
+    floatx4 acc[KW][CW][NT];
+#pragma unroll
+    for (int i = 0; i < KW; ++i)
+#pragma unroll
+        for (int j = 0; j < CW; ++j)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[i][j][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (item < a.items) {
+        const int strip = item % a.nstrip;
+        const int t2 = item / a.nstrip;
+        const int seg = t2 % a.nseg, n = t2 / a.nseg;
+        const int ch = lane & 15, pj = lane >> 4;
+        const int q1 = strip * 16 + 4 * pj;  // first output column of the lane's 4 pixels
+        const int PQ = a.P * a.Q, HW = a.H * a.W;
+        const __amdgpu_buffer_rsrc_t rd = rows_rsrc(dy + (int64_t)n * a.K * PQ, a.K * PQ * 4);
+        const __amdgpu_buffer_rsrc_t rx = rows_rsrc(x + (int64_t)n * a.C * HW, a.C * HW * 4);
+        // per-lane channel bases (or kOob for channels past K / C)
+        uint32_t dbase[KW], xbase[CW];
+#pragma unroll
+        for (int i = 0; i < KW; ++i) {
+            const int k = kg * 16 * KW + 16 * i + ch;
+            dbase[i] = k < a.K ? (uint32_t)k * (uint32_t)PQ * 4u : kOob;
+        }
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            const int c = cg * 16 * CW + 16 * j + ch;
+            xbase[j] = c < a.C ? (uint32_t)c * (uint32_t)HW * 4u : kOob;
+        }
+        const int pw = VEC ? PW : a.pw;
+        const int col0 = SH * q1 - pw;  // x column of span element 0
+        const int p0 = seg * a.RB;
+        auto load_dy = [&](float (&dv)[KW][4], int p) __attribute__((always_inline)) {
+            const bool prow = p < a.P && p < p0 + a.RB;
+#pragma unroll
+            for (int i = 0; i < KW; ++i) {
+                if constexpr (VEC) {
+                    const uint32_t off =
+                        (prow && q1 < a.Q && dbase[i] != kOob) ? dbase[i] + (uint32_t)(p * a.Q + q1) * 4u : kOob;
+                    const floatx4 v = wg_ld4(rd, off);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) dv[i][m] = v[m];
+                } else {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const uint32_t off = (prow && q1 + m < a.Q && dbase[i] != kOob)
+                                                 ? dbase[i] + (uint32_t)(p * a.Q + q1 + m) * 4u
+                                                 : kOob;
+                        dv[i][m] = wg_ld1(rd, off);
+                    }
+                }
+            }
+        };
+        auto load_x = [&](float (&xv)[CW][SPAN], int h) __attribute__((always_inline)) {
+            const bool hrow = h >= 0 && h < a.H;
+            const uint32_t rowoff = (uint32_t)(hrow ? h : 0) * (uint32_t)a.W * 4u;
+#pragma unroll
+            for (int j = 0; j < CW; ++j) {
+                const bool ok = hrow && xbase[j] != kOob;
+                const uint32_t b = xbase[j] + rowoff;
+                if constexpr (VEC) {
+#pragma unroll
+                    for (int i = 0; i < PW; ++i) {
+                        const int col = col0 + i;
+                        xv[j][i] = wg_ld1(rx, (ok && col >= 0 && col < a.W) ? b + (uint32_t)col * 4u : kOob);
+                    }
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        const int col = SH * q1 + 4 * u;  // a multiple of 4; W % 4 == 0
+                        const floatx4 v = wg_ld4(rx, (ok && col < a.W) ? b + (uint32_t)col * 4u : kOob);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) xv[j][PW + 4 * u + e] = v[e];
+                    }
+#pragma unroll
+                    for (int i = 0; i < NTAIL; ++i) {
+                        const int col = SH * q1 + 4 * NB + i;
+                        xv[j][PW + 4 * NB + i] = wg_ld1(rx, (ok && col < a.W) ? b + (uint32_t)col * 4u : kOob);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < SPAN; ++i) {
+                        const int col = col0 + i;
+                        xv[j][i] = wg_ld1(rx, (ok && col >= 0 && col < a.W) ? b + (uint32_t)col * 4u : kOob);
+                    }
+                }
+            }
+        };
+        auto mfmas = [&](const float (&dv)[KW][4], const float (&x0)[CW][SPAN], const float (&x1)[CW][SPAN],
+                         const float (&x2)[CW][SPAN]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int s = 0; s < S; ++s)
+#pragma unroll
+                        for (int i = 0; i < KW; ++i)
+#pragma unroll
+                            for (int j = 0; j < CW; ++j) {
+                                const float bv = r == 0 ? x0[j][SH * m + s] : r == 1 ? x1[j][SH * m + s]
+                                                                                     : x2[j][SH * m + s];
+                                acc[i][j][r * S + s] =
+                                    __builtin_amdgcn_mfma_f32_16x16x4f32(dv[i][m], bv, acc[i][j][r * S + s], 0, 0, 0);
+                            }
+        };
+        float dv[2][KW][4];
+        if constexpr (RING) {
+            // x rows p - ph + r (r = 0..2) of output row p live in ring slots (p - p0 + r) & 3
+            float xr[4][CW][SPAN];
+            const int hb = p0 - a.ph;
+            load_x(xr[0], hb);
+            load_x(xr[1], hb + 1);
+            load_x(xr[2], hb + 2);
+            load_dy(dv[0], p0);
+            for (int jb = 0; jb < a.RB; jb += 4) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    load_x(xr[(j + 3) & 3], hb + jb + j + 3);
+                    load_dy(dv[(j + 1) & 1], p0 + jb + j + 1);
+                    mfmas(dv[j & 1], xr[j & 3], xr[(j + 1) & 3], xr[(j + 2) & 3]);
+                }
+            }
+        } else {
+            float xs[2][R][CW][SPAN];
+#pragma unroll
+            for (int r = 0; r < R; ++r) load_x(xs[0][r], p0 * SH - a.ph + r);
+            load_dy(dv[0], p0);
+            for (int jb = 0; jb < a.RB; jb += 2) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int pn = p0 + jb + j + 1;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) load_x(xs[(j + 1) & 1][r], pn * SH - a.ph + r);
+                    load_dy(dv[(j + 1) & 1], pn);
+                    mfmas(dv[j & 1], xs[j & 1][0], xs[j & 1][R > 1 ? 1 : 0], xs[j & 1][R > 2 ? 2 : 0]);
+                }
+            }
+        }
+    }
+    // block partial part[g][bi][kk][cc][t] (kk < 16 KW, cc < 16 CW): the 4 waves' tiles summed
+    // in wave order, one (KW, CW) tile pair at a time through LDS
+    constexpr int KT = 16 * KW, CT = 16 * CW, PER = KT * CT * NT;
+    float* out = part + ((int64_t)g * a.bpg + bi) * PER;
+#pragma unroll
+    for (int i = 0; i < KW; ++i)
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            if (i + j) __syncthreads();  // the previous pair's reads are done
+#pragma unroll
+            for (int t = 0; t < NT; ++t) red[wave][t][lane] = acc[i][j][t];
+            __syncthreads();
+            for (int e = threadIdx.x; e < 256 * NT; e += 256) {
+                // e = (kl * 16 + cl) * NT + t; MFMA D layout: lane (kl >> 2) * 16 + cl, element kl & 3
+                const int t = e % NT, cl = (e / NT) & 15, kl = e / (NT * 16);
+                const int ln = ((kl >> 2) << 4) + cl, v = kl & 3;
+                float sum = 0.0f;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) sum += red[w][t][ln][v];
+                out[((16 * i + kl) * CT + 16 * j + cl) * NT + t] = sum;
+            }
+        }
+}
+
+// dW[k][c][t] = sum over the channel group's block partials, in block order.  Block =
+// 64 consecutive partial elements x 16 slices of the partial list (1024 threads); the 16
+// slice sums are added in slice order.
+__global__ __launch_bounds__(1024) void wgrad2_reduce(const float* __restrict__ part, float* __restrict__ dw, int K,
+                                                      int C, int NT, int KT, int CT, int CG, int bpg) {
+    __shared__ float red[16][64];
+    const int PER = KT * CT * NT;
+    const int chunks = (PER + 63) / 64;
+    const int g = blockIdx.x / chunks;
+    const int e = (blockIdx.x - g * chunks) * 64 + (threadIdx.x & 63);
+    const int sl = threadIdx.x >> 6;
+    float v = 0.0f;
+    if (e < PER) {
+        const float* src = part + (int64_t)g * bpg * PER + e;
+        for (int b = sl; b < bpg; b += 16) v += src[(int64_t)b * PER];
+    }
+    red[sl][threadIdx.x & 63] = v;
+    __syncthreads();
+    if (sl == 0 && e < PER) {
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sum += red[i][threadIdx.x];
+        const int t = e % NT, cc = (e / NT) % CT, kk = e / (NT * CT);
+        const int kg = g / CG, cg = g - kg * CG;
+        const int k = kg * KT + kk, c = cg * CT + cc;
+        if (k < K && c < C) dw[((int64_t)k * C + c) * NT + t] = sum;
+    }
+}
+
 bool wgrad_plan(WgradArgs& a, size_t& lds, size_t& part_bytes) {
     if (!((a.R == 3 && a.S == 3) || (a.R == 1 && a.S == 1))) return false;
     a.KT = (a.K + 15) / 16;
@@ -185,6 +430,72 @@ hipError_t launch_wgrad(const WgradArgs& a0, const float* x, const float* dy, fl
     return hipGetLastError();
 }
 
+// Register-streaming plan: dilation 1, sh == sw in {1, 2}, 1x1 (pad 0) or 3x3 kernels.
+// Rows per segment: the largest multiple of 4 that still gives >= 4096 waves in total
+// (16 per CU), at least 4.
+bool wgrad2_plan(Wgrad2Args& a, int R, int S, int sh, int sw, int dh, int dw, int& SH, int& KW, int& CW, bool& vec,
+                 size_t& part_bytes) {
+    if (dh != 1 || dw != 1 || sh != sw || (sh != 1 && sh != 2)) return false;
+    if (!((R == 3 && S == 3) || (R == 1 && S == 1))) return false;
+    SH = sh;
+    KW = a.K > 16 ? 2 : 1;
+    CW = a.C > 16 ? 2 : 1;
+    const int pwv = R == 3 ? 1 : 0;
+    vec = a.W % 4 == 0 && a.Q % 4 == 0 && a.pw == pwv;
+    a.KG = (a.K + 16 * KW - 1) / (16 * KW);
+    a.CG = (a.C + 16 * CW - 1) / (16 * CW);
+    a.nstrip = (a.Q + 15) / 16;
+    const int64_t per_seg = (int64_t)a.KG * a.CG * a.N * a.nstrip;
+    const int P4 = (a.P + 3) / 4 * 4;
+    int rb = 4;
+    for (int c = P4; c >= 4; c -= 4) {
+        const int64_t nseg = (a.P + c - 1) / c;
+        if (per_seg * nseg >= 4096) { rb = c; break; }
+    }
+    a.RB = rb;
+    a.nseg = (a.P + rb - 1) / rb;
+    const int64_t items = (int64_t)a.N * a.nseg * a.nstrip;
+    if (items > INT32_MAX / 4) return false;
+    a.items = (int)items;
+    a.bpg = (a.items + 3) / 4;
+    part_bytes = (size_t)a.KG * a.CG * a.bpg * (16 * KW) * (16 * CW) * R * S * sizeof(float);
+    return true;
+}
+
+template <int R, int S, int SH, int PW, int KW, int CW>
+void launch_wgrad2_t(bool vec, const Wgrad2Args& a, const float* x, const float* dy, float* part, hipStream_t st) {
+    const dim3 grid((unsigned)(a.KG * a.CG * a.bpg));
+    if (vec)
+        hipLaunchKernelGGL((wgrad2_f32<R, S, SH, PW, KW, CW, true>), grid, dim3(256), 0, st, x, dy, part, a);
+    else
+        hipLaunchKernelGGL((wgrad2_f32<R, S, SH, PW, KW, CW, false>), grid, dim3(256), 0, st, x, dy, part, a);
+}
+
+template <int R, int S, int SH, int PW>
+void launch_wgrad2_k(int KW, int CW, bool vec, const Wgrad2Args& a, const float* x, const float* dy, float* part,
+                     hipStream_t st) {
+    if (KW == 1 && CW == 1) launch_wgrad2_t<R, S, SH, PW, 1, 1>(vec, a, x, dy, part, st);
+    else if (KW == 2 && CW == 1) launch_wgrad2_t<R, S, SH, PW, 2, 1>(vec, a, x, dy, part, st);
+    else if (KW == 1 && CW == 2) launch_wgrad2_t<R, S, SH, PW, 1, 2>(vec, a, x, dy, part, st);
+    else launch_wgrad2_t<R, S, SH, PW, 2, 2>(vec, a, x, dy, part, st);
+}
+
+hipError_t launch_wgrad2(const Wgrad2Args& a, int R, int SH, int KW, int CW, bool vec, const float* x, const float* dy,
+                         float* dw, float* part, hipStream_t st) {
+    if (R == 3 && SH == 1) launch_wgrad2_k<3, 3, 1, 1>(KW, CW, vec, a, x, dy, part, st);
+    else if (R == 3 && SH == 2) launch_wgrad2_k<3, 3, 2, 1>(KW, CW, vec, a, x, dy, part, st);
+    else if (R == 1 && SH == 1) launch_wgrad2_k<1, 1, 1, 0>(KW, CW, vec, a, x, dy, part, st);
+    else if (R == 1 && SH == 2) launch_wgrad2_k<1, 1, 2, 0>(KW, CW, vec, a, x, dy, part, st);
+    else return hipErrorInvalidValue;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int KT = 16 * KW, CT = 16 * CW, NT = R * R;
+    const int chunks = (KT * CT * NT + 63) / 64;
+    hipLaunchKernelGGL(wgrad2_reduce, dim3((unsigned)(a.KG * a.CG * chunks)), dim3(1024), 0, st, part, dw, a.K, a.C,
+                       NT, KT, CT, a.CG, a.bpg);
+    return hipGetLastError();
+}
+
 }  // namespace po2q
 
 namespace {
@@ -216,6 +527,29 @@ bool wgrad_setup(po2q::WgradArgs& a, size_t& lds, size_t& part, int64_t N, int64
     return true;
 }
 
+// The register-streaming kernel where it applies (PO2Q_WGRAD=1 forces the LDS-band kernel)
+struct Wgrad2Choice {
+    bool use = false;
+    po2q::Wgrad2Args a;
+    int R = 0, SH = 0, KW = 0, CW = 0;
+    bool vec = false;
+    size_t part = 0;
+};
+
+Wgrad2Choice wgrad2_choose(const po2q::WgradArgs& a1) {
+    Wgrad2Choice c;
+    static const int force1 = [] {
+        const char* e = getenv("PO2Q_WGRAD");
+        return e ? atoi(e) : 0;
+    }();
+    if (force1 == 1) return c;
+    po2q::Wgrad2Args& a = c.a;
+    a.N = a1.N; a.C = a1.C; a.H = a1.H; a.W = a1.W; a.K = a1.K; a.P = a1.P; a.Q = a1.Q; a.ph = a1.ph; a.pw = a1.pw;
+    c.use = po2q::wgrad2_plan(a, a1.R, a1.S, a1.sh, a1.sw, a1.dh, a1.dw, c.SH, c.KW, c.CW, c.vec, c.part);
+    c.R = a1.R;
+    return c;
+}
+
 }  // namespace
 
 size_t po2q_qconv2d_wgrad_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
@@ -225,7 +559,8 @@ size_t po2q_qconv2d_wgrad_workspace_bytes(int64_t N, int64_t C, int64_t H, int64
     size_t lds, part;
     if (!wgrad_setup(a, lds, part, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups))
         return 0;
-    return std::max<size_t>(part, 256);
+    const Wgrad2Choice c2 = wgrad2_choose(a);
+    return std::max<size_t>(c2.use ? c2.part : part, 256);
 }
 
 int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw, int64_t N, int64_t C, int64_t H, int64_t W,
@@ -240,12 +575,17 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw, int64_t N
         po2q::set_error("po2q: null pointer");
         return PO2Q_ERR_INVALID;
     }
+    const Wgrad2Choice c2 = wgrad2_choose(a);
+    if (c2.use) part = c2.part;
     if (workspace_bytes < part) {
         po2q::set_error("po2q: wgrad workspace too small (need " + std::to_string(part) + " bytes)");
         return PO2Q_ERR_WORKSPACE;
     }
-    const hipError_t e = po2q::launch_wgrad(a, x, dy, dw, reinterpret_cast<float*>(workspace), lds,
-                                            reinterpret_cast<hipStream_t>(stream));
+    const hipError_t e =
+        c2.use ? po2q::launch_wgrad2(c2.a, c2.R, c2.SH, c2.KW, c2.CW, c2.vec, x, dy, dw,
+                                     reinterpret_cast<float*>(workspace), reinterpret_cast<hipStream_t>(stream))
+               : po2q::launch_wgrad(a, x, dy, dw, reinterpret_cast<float*>(workspace), lds,
+                                    reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {
         po2q::set_error(std::string("po2q: wgrad launch: ") + hipGetErrorString(e));
         return PO2Q_ERR_HIP;

@@ -31,6 +31,10 @@ from .. import _lib
 from ..utils.quantizers import NATIVE_MODES
 
 
+# False: every backward is one aten.convolution_backward of Q(w) (for A/B measurements)
+NATIVE_BACKWARD = True
+
+
 class _QConv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, bits, mode, precision):
@@ -59,9 +63,9 @@ class _QConv2dFn(torch.autograd.Function):
         need_b = bias is not None and ctx.needs_input_grad[2]
         R, S = weight.shape[2], weight.shape[3]
         pad = _lib._pair(padding)
-        native_x = (need_x and tuple(_lib._pair(stride)) == (1, 1) and tuple(_lib._pair(dilation)) == (1, 1)
+        native_x = (NATIVE_BACKWARD and need_x and tuple(_lib._pair(stride)) == (1, 1) and tuple(_lib._pair(dilation)) == (1, 1)
                     and groups == 1 and pad[0] <= R - 1 and pad[1] <= S - 1)
-        native_w = need_w and _lib.wgrad_supported(weight.shape, groups)
+        native_w = NATIVE_BACKWARD and need_w and _lib.wgrad_supported(weight.shape, groups)
         gx = gw = gb = None
         if native_x:
             wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()

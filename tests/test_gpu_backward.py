@@ -93,3 +93,33 @@ def test_wgrad_deterministic_and_unsupported():
     assert not _lib.wgrad_supported((16, 32, 5, 5), 1) and not _lib.wgrad_supported((16, 8, 3, 3), 4)
     with pytest.raises(_lib.Po2qError):
         _lib.conv_wgrad(x, gy, (16, 32, 5, 5), 1, 2)
+
+
+WGRAD_SHAPES = [  # N, C, H, W, K, R, stride, pad, dilation
+    (2, 3, 32, 32, 16, 3, 1, 1, 1),     # stem: C = 3
+    (3, 16, 33, 30, 16, 3, 1, 1, 1),    # ragged rows, Q % 4 != 0 (scalar loads)
+    (2, 48, 20, 20, 80, 3, 1, 1, 1),    # C, K past one 32-channel group, not multiples of 32
+    (2, 16, 31, 31, 32, 3, 2, 1, 1),    # stride 2, odd sizes
+    (2, 32, 28, 28, 64, 3, 2, 1, 1),    # stride 2, W % 4 == 0
+    (2, 64, 14, 14, 16, 1, 1, 0, 1),    # 1x1 stride 1
+    (2, 32, 15, 15, 64, 1, 2, 0, 1),    # 1x1 stride 2, ragged
+    (2, 16, 12, 12, 16, 3, 1, 0, 1),    # 3x3 no padding
+    (2, 16, 12, 12, 16, 3, 1, 2, 1),    # 3x3 padding 2
+    (2, 16, 16, 16, 16, 3, 1, 2, 2),    # dilation 2 (LDS-band kernel)
+    (1, 16, 8, 8, 16, 3, 1, 1, 1),      # fewer items than one block
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES, ids=[str(s) for s in WGRAD_SHAPES])
+def test_wgrad_kernels_vs_torch_fp64(shape):
+    N, C, H, W, K, R, st, pad, dil = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, generator=g)
+    P = (H + 2 * pad - dil * (R - 1) - 1) // st + 1
+    Q = (W + 2 * pad - dil * (R - 1) - 1) // st + 1
+    gy = torch.randn(N, K, P, Q, generator=g)
+    gw = _lib.conv_wgrad(x.to(DEV), gy.to(DEV), (K, C, R, R), st, pad, dil, 1)
+    _, rw, _ = torch.ops.aten.convolution_backward(gy.double(), x.double(), torch.zeros(K, C, R, R, dtype=torch.float64),
+                                                   None, [st, st], [pad, pad], [dil, dil], False, [0, 0], 1,
+                                                   [False, True, False])
+    assert nerr(gw, rw) <= CONV_TOL, nerr(gw, rw)

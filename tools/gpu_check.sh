@@ -43,6 +43,10 @@ for s in $STEPS; do
                 run models_c4 300 python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
         profmb) run profmb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profmb -o run \
                   -- python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --only-fused ;;
+        bwdtests) run bwdtests 600 python -u -m pytest tests/test_gpu_backward.py tests/test_qat.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/bwdtests.log || grep -q "failed\|error" gpurun_out/bwdtests.log; then
+                   echo "stopping: backward GPU tests did not pass"; exit 1
+               fi ;;
         bwd) run bwd224 600 python tools/bwd_bench.py --batch 64
              run bwd32 600 python tools/bwd_bench.py --batch 256 --image 32
              run qatb 600 python tools/qat_bench.py resnet56 ;;

@@ -45,12 +45,20 @@ def run(model_type, qn, bits, bs, steps=20, warmup=5):
 
 
 def main():
-    torch.backends.cudnn.benchmark = os.environ.get("QAT_BENCH_FIND", "1") == "1"  # MIOpen find + po2q autotune
+    # MIOpen find (QAT_BENCH_FIND=1) and the po2q autotuner (always)
+    torch.backends.cudnn.benchmark = os.environ.get("QAT_BENCH_FIND", "0") == "1"
+    from po2_quantization_amd import _lib
+    _lib.benchmark = True
     only = sys.argv[1:]  # e.g. `qat_bench.py resnet56`
     for model_type, qn, bits in (("resnet56", "po2", 4), ("resnet20", "po2", 4)):
         if only and model_type not in only:
             continue
         ms, ips = run(model_type, qn, bits, 256)
+        QC.NATIVE_BACKWARD = False
+        try:
+            ms_a, ips_a = run(model_type, qn, bits, 256)
+        finally:
+            QC.NATIVE_BACKWARD = True
         orig = QC.QuantizedConv2d.forward
         QC.QuantizedConv2d.forward = torch_forward
         try:
@@ -59,6 +67,8 @@ def main():
             QC.QuantizedConv2d.forward = orig
         print(json.dumps({"model": model_type, "quantizer": qn, "bits": bits, "batch": 256, "image": 32,
                           "native_ms_per_step": round(ms, 3), "native_images_per_s": round(ips, 1),
+                          "aten_backward_ms_per_step": round(ms_a, 3), "aten_backward_images_per_s": round(ips_a, 1),
+                          "miopen_find": torch.backends.cudnn.benchmark,
                           "torch_forward_ms_per_step": round(ms_t, 3),
                           "torch_forward_images_per_s": round(ips_t, 1)}), flush=True)
 
