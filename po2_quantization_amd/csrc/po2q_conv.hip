@@ -261,7 +261,7 @@ static bool tuned_lookup(ConvPlan& p, int mode, int bits, int fsr, int flags) {
     return true;
 }
 
-static bool plan_fallback(ConvPlan& p);
+static bool plan_fallback(ConvPlan& p, bool dw3 = true);
 
 // Heuristic plan + the ranked bf16x3 alternatives (empty unless bf16x3 applies).
 static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, std::vector<PlanCand>* reg_out,
@@ -326,6 +326,12 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
     if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma, &rows)) return false;
     out.clear();
     out.push_back(p);
+    if (p.kind == KIND_DEPTHWISE && p.vrx == 1) {  // the one-output-per-lane kernel as the alternative
+        ConvPlan l;
+        const bool ok = plan_geometry(l, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups) &&
+                        plan_fallback(l, false);
+        if (ok && l.vrx == 0) out.push_back(l);
+    }
     auto add = [&](const std::vector<PlanCand>& v, int n) {
         for (int i = 0; i < (int)v.size() && i < n; ++i) {
             const ConvPlan& c = v[i].plan;
@@ -343,10 +349,13 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
     return true;
 }
 
-static bool plan_fallback(ConvPlan& p) {
+static bool plan_fallback(ConvPlan& p, bool dw3) {
     const int N = p.N, K = p.K, R = p.R, S = p.S, P = p.P, Q = p.Q, groups = p.groups;
     if (p.Cg == 1 && groups > 1) {  // depthwise
+        const char* legacy = getenv("PO2Q_DW_LEGACY");
+        if (dw3 && !(legacy && legacy[0] == '1') && dw3_plan(p)) return true;
         p.kind = KIND_DEPTHWISE;
+        p.vrx = 0;
         p.MI = p.NJ = 1;
         p.TP = p.TQ = p.tilesP = p.tilesQ = 1;
         p.CC = 1; p.nchunks = 1; p.kblocks = 1;
@@ -434,6 +443,8 @@ static hipError_t launch_mfma_nj(const ConvPlan& p, const float* x, const float*
 
 hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
                        hipStream_t s) {
+    if (p.kind == KIND_DEPTHWISE && p.vrx == 1)
+        return launch_conv_dw3(p, x, packed, bias, y, nullptr, nullptr, nullptr, 0, s);
     if (p.kind == KIND_DEPTHWISE) {
         hipLaunchKernelGGL(conv_depthwise, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
                            to_args(p));

@@ -109,6 +109,12 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
                               int bits, int fsr, int mode, uint16_t* packed, float* scale_out,
                               hipStream_t s);
 
+// Depthwise 3x3 LDS-halo kernel (po2q_conv_dw.hip): plan (kind KIND_DEPTHWISE, vrx 1) and launch
+// with the fused epilogue (ps / pb / res may be NULL, act PO2Q_ACT_*).
+bool dw3_plan(ConvPlan& p);
+bool dw3_plan_ok(const ConvPlan& p);
+hipError_t launch_conv_dw3(const ConvPlan& p, const float* x, const float* qw, const float* bias, float* y,
+                           const float* ps, const float* pb, const float* res, int act, hipStream_t s);
 hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, const float* bias,
                        float* y, hipStream_t s);
 

@@ -47,6 +47,11 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/bwdtests.log || grep -q "failed\|error" gpurun_out/bwdtests.log; then
                    echo "stopping: backward GPU tests did not pass"; exit 1
                fi ;;
+        dwtests) run dwtests 600 python -u -m pytest tests/test_gpu_depthwise.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/dwtests.log || grep -q "failed\|error" gpurun_out/dwtests.log; then
+                   echo "stopping: depthwise GPU tests did not pass"; exit 1
+               fi ;;
+        dwb) run dwb 300 python tools/dw_bench.py ;;
         bwd) run bwd224 600 python tools/bwd_bench.py --batch 64
              run bwd32 600 python tools/bwd_bench.py --batch 256 --image 32
              run qatb 600 python tools/qat_bench.py resnet56 ;;
