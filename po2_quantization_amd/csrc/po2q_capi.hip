@@ -113,7 +113,8 @@ struct WsLayout {
 static WsLayout ws_layout(const ConvPlan& p, int mode) {
     WsLayout L;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) &&
+    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS ||
+                        p.kind == KIND_DEPTHWISE) &&
                        nw <= kFusedAbsmaxMax;
     L.nparts = (mode == PO2Q_MODE_NONE || fused) ? 0 : absmax_blocks(nw);
     L.part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));

@@ -7,6 +7,8 @@
 //                               scale, then quantizes a grid-stride slice
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "po2q_internal.h"
 #include "po2q_quant_dev.h"
 
@@ -66,6 +68,29 @@ __global__ __launch_bounds__(kThreads) void quantize_plain_kernel(const float* _
     const float scale = fold_scale(partial, nparts, red4);
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+        out[i] = quantize_elem(w[i], scale, mode, lo, hi);
+}
+
+// Small tensors (depthwise weights, <= kFusedAbsmaxMax elements): absmax and quantize in one
+// launch -- every block reduces the whole L2-resident tensor, then quantizes its slice.
+__global__ __launch_bounds__(1024) void quantize_plain_fused_kernel(const float* __restrict__ w, int n, int lo, int hi,
+                                                                    int mode, float* __restrict__ out) {
+    __shared__ unsigned red[16];
+    unsigned m = 0u;
+    constexpr int U = 4;  // independent loads in flight per thread
+    for (int i = threadIdx.x; i < n; i += U * 1024) {
+        unsigned v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = i + u * 1024;
+            v[u] = k < n ? (__float_as_uint(w[k]) & 0x7fffffffu) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) m = max(m, v[u]);
+    }
+    m = block_max_u32<16>(m, red);
+    const float scale = __uint_as_float(m);
+    for (int i = blockIdx.x * 1024 + threadIdx.x; i < n; i += gridDim.x * 1024)
         out[i] = quantize_elem(w[i], scale, mode, lo, hi);
 }
 
@@ -276,6 +301,12 @@ hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned
     if (p.kind == KIND_DEPTHWISE) {  // depthwise: plain [K][1][R][S] quantized copy
         const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
         if (mode == 0) return hipMemcpyAsync(packed, w, n * sizeof(float), hipMemcpyDeviceToDevice, s);
+        if (nparts == 0) {  // fused absmax (small tensor)
+            const int b = (int)std::min<int64_t>(8, (n + 4095) / 4096);
+            hipLaunchKernelGGL(quantize_plain_fused_kernel, dim3(b), dim3(1024), 0, s, w, (int)n, lo, hi, mode - 1,
+                               packed);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL(quantize_plain_kernel, dim3(grid_for(n)), dim3(kThreads), 0, s, w, n, partial, nparts,
                            lo, hi, mode - 1, packed);
         return hipGetLastError();
