@@ -74,10 +74,19 @@ class QConvChain:
         self.mode, self.bits, self.precision = mode, bits, precision
         self.timed_layer = None      # index of the layer whose launches are timed
         self.events = []
+        self.pair = True             # conv1 -> conv2 of stage-1 blocks as one pair launch
 
     def conv(self, i, x):
         _, C, K, R, st, pad, _ = self.layers[i]
         return _lib.qconv2d(x, self.weights[i], None, st, pad, 1, 1, self.bits, self.mode, 1, self.precision)
+
+    def pairable(self, i, x):
+        """conv1 -> conv2 of block i as ONE launch (po2q_qconv2d_pair_f32): both 3x3 s1 16->16."""
+        if not self.pair:
+            return False
+        (_, C1, K1, R1, s1, _, _), (_, C2, K2, R2, s2, _, _) = self.layers[i], self.layers[i + 1]
+        return (C1, K1, C2, K2, R1, R2, s1, s2) == (16, 16, 16, 16, 3, 3, 1, 1) and self.mode in ("po2", "po2+") \
+            and _lib.pair_supported(x.shape, self.bits, self.mode)
 
     def forward(self, x, record=False):
         i = 0
@@ -85,8 +94,11 @@ class QConvChain:
             name, _, _, _, _, _, role = self.layers[i]
             assert role == "conv1"
             has_ds = i + 2 < len(self.layers) and self.layers[i + 2][6] == "ds"
-            out = self._timed(i, x, record)
-            out = self._timed(i + 1, out, record)
+            if self.pairable(i, x):
+                out = self._timed_pair(i, x, record)
+            else:
+                out = self._timed(i, x, record)
+                out = self._timed(i + 1, out, record)
             if has_ds:
                 self._timed(i + 2, x, record)  # projection shortcut (its output feeds the add)
                 i += 3
@@ -95,6 +107,20 @@ class QConvChain:
             x = out
         pooled = x.mean(dim=(2, 3))
         return torch.nn.functional.linear(pooled, self.fc_w, self.fc_b)
+
+    def pair_call(self, i, x):
+        return _lib.qconv2d_pair(x, self.weights[i], self.weights[i + 1], self.bits, self.mode)
+
+    def _timed_pair(self, i, x, record):
+        if record and i + 1 == self.timed_layer:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            y = self.pair_call(i, x)
+            e1.record()
+            self.events.append((e0, e1))
+            return y
+        return self.pair_call(i, x)
 
     def _timed(self, i, x, record):
         # HIP events around the timed layer itself (one per step: an event pair costs
@@ -218,6 +244,8 @@ def main():
     ap.add_argument("--precision", default="auto", choices=["auto", "fp32", "bf16x3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pair", action="store_true",
+                    help="run every conv as its own launch (no stage-1 conv1->conv2 pair kernel)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="use the heuristic plans instead of autotuning each conv shape on first use")
     args = ap.parse_args()
@@ -242,6 +270,7 @@ def main():
     n_blocks = {"resnet20": 3, "resnet32": 5, "resnet44": 7, "resnet56": 9}[args.model]
     chain = QConvChain(n_blocks, args.classes, args.quantizer, args.bits, args.precision, dev, seed=0)
     chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
+    chain.pair = not args.no_pair
     B, Hs = args.batch, args.image
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
     gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
@@ -270,32 +299,43 @@ def main():
         dt = timed_steps(gstep if graph is not None else step, args.steps,
                          max(args.warmup, 1 if _lib.benchmark else 0), world, torch.cuda.synchronize, dev)
 
-    # dominant op: fused quantize+conv of the timed shape, HIP events on its stream
-    if graph is not None:
-        # per-launch time from a graph of back-to-back launches of that layer alone
+    # dominant op (HIP events on its stream): the stage-1 conv pair (conv1 -> conv2 of a block
+    # in one launch) when the chain runs pairs, else the fused quantize+conv of the timed shape
+    pair_used = chain.pairable(0, x)
+    xl = torch.relu(torch.randn(args.batch, 16, args.image, args.image, device=dev))
+
+    def launch_avg_ms(fn, reps=20):
+        """Average duration of `fn` from back-to-back launches: a HIP graph of `reps` launches
+        replayed 5 times (--graph), else `reps` launches bracketed by events."""
         with torch.no_grad():
-            _, C0, _, _, _, _, _ = chain.layers[chain.timed_layer]
-            xl = torch.relu(torch.randn(args.batch, C0, args.image, args.image, device=dev))
-            reps = 20
-            chain.conv(chain.timed_layer, xl)
+            fn()
             torch.cuda.synchronize()
-            lg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(lg):
-                for _ in range(reps):
-                    chain.conv(chain.timed_layer, xl)
-            lg.replay()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(5):
+            if graph is not None:
+                lg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(lg):
+                    for _ in range(reps):
+                        fn()
                 lg.replay()
+                e0.record()
+                for _ in range(5):
+                    lg.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / (5 * reps)
+            e0.record()
+            for _ in range(reps):
+                fn()
             e1.record()
             torch.cuda.synchronize()
-            chain.events = [(e0, e1)]
-            ev_scale = 1.0 / (5 * reps)
+            return e0.elapsed_time(e1) / reps
+
+    if graph is not None:
+        avg_ms = launch_avg_ms((lambda: chain.pair_call(0, xl)) if pair_used else
+                               (lambda: chain.conv(chain.timed_layer, xl)))
     else:
-        ev_scale = 1.0
-    ev_ms = [a.elapsed_time(b) * ev_scale for a, b in chain.events]
-    avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
+        ev_ms = [a.elapsed_time(b) for a, b in chain.events]
+        avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
     _, C, K, R, st, pad, _ = chain.layers[chain.timed_layer]
     flops, nbytes = conv_work(B, C, Hs, K, R, st, pad)
     # the conv arithmetic the library actually planned for this layer (AUTO picks
@@ -303,30 +343,50 @@ def main():
     plan = _lib.describe(B, C, Hs, Hs, K, R, R, st, pad, 1, 1, args.bits,
                          None if args.quantizer == "none" else args.quantizer, 1, args.precision)
     prec = "bf16x3" if "kind=bf16x3" in plan else "fp32"
-    if prec == "bf16x3":
-        peak_c = PEAK_BF16_MFMA_TFLOPS / 3.0
-    else:
-        peak_c = PEAK_FP32_MFMA_TFLOPS
-    hbm_bound = flops / nbytes * PEAK_HBM_GBS / 1e3 < peak_c  # TFLOP/s attainable from HBM
-    if hbm_bound:
-        achieved = nbytes / (avg_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4)}
-    else:
-        achieved = flops / (avg_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak_c, 1), "unit": "TFLOP/s",
+    peak_c = PEAK_BF16_MFMA_TFLOPS / 3.0 if prec == "bf16x3" else PEAK_FP32_MFMA_TFLOPS
+
+    def roofline(fl, nb, ms):
+        if fl / nb * PEAK_HBM_GBS / 1e3 < peak_c:  # TFLOP/s attainable from HBM below the MFMA peak
+            achieved = nb / (ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 4)}
+        achieved = fl / (ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak_c, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak_c, 4)}
-    roof["traffic"] = None
-    traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(traffic_file):
-        try:
-            tr = json.load(open(traffic_file)).get(plan)
-            roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
-        except (ValueError, OSError):
-            pass
-    roof.update({"kernel": "fused %s quantize+conv %dx%d %d->%d @%dx%d bs=%d (pack + conv launches): %s"
-                           % (args.quantizer, R, R, C, K, Hs, Hs, B, plan),
-                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(nbytes), "flops": int(flops)})
+
+    def traffic_of(key):
+        traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(traffic_file):
+            try:
+                tr = json.load(open(traffic_file)).get(key)
+                return tr.get("hbm_bytes_per_launch") if tr else None
+            except (ValueError, OSError):
+                return None
+        return None
+
+    layer_kernel = ("fused %s quantize+conv %dx%d %d->%d @%dx%d bs=%d: %s"
+                    % (args.quantizer, R, R, C, K, Hs, Hs, B, plan))
+    if pair_used:
+        # x in + y out + both weights read twice (absmax + staging); 2 convs of flops
+        pflops, pbytes = 2 * flops, 4.0 * (2 * B * 16 * Hs * Hs + 4 * 16 * 16 * 9)
+        roof = roofline(pflops, pbytes, avg_ms)
+        roof["traffic"] = traffic_of("pair16 %dx%d bs=%d" % (Hs, Hs, B))
+        roof.update({"kernel": "conv_pair16 (po2q_qconv2d_pair_f32): layer1.0 conv1 -> conv2, 2 fused %s quantize+"
+                               "conv 3x3 16->16 @%dx%d bs=%d in one launch, intermediate on chip"
+                               % (args.quantizer, Hs, Hs, B),
+                     "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(pbytes), "flops": int(pflops)})
+        # the single-layer kernel of the same shape (used wherever pairs do not apply)
+        lms = launch_avg_ms(lambda: chain.conv(chain.timed_layer, xl))
+        layer_roof = roofline(flops, nbytes, lms)
+        layer_roof["traffic"] = traffic_of(plan)
+        layer_roof.update({"kernel": layer_kernel, "avg_launch_ms": round(lms, 4), "algorithmic_bytes": int(nbytes),
+                           "flops": int(flops)})
+    else:
+        roof = roofline(flops, nbytes, avg_ms)
+        roof["traffic"] = traffic_of(plan)
+        roof.update({"kernel": layer_kernel, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(nbytes),
+                     "flops": int(flops)})
+        layer_roof = None
 
     images = world * B * args.steps
     out = {
@@ -334,14 +394,17 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
-        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s"
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
+                                  " (stage-1 conv1->conv2 pairs as one launch each)" if pair_used else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
+                   "conv_pairs": pair_used,
                    "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
                    "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world, "world_size": world,
                    "hip_graph": graph is not None},
         "roofline": roof,
+        "layer_roofline": layer_roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -233,6 +233,25 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw,
                            int64_t dil_h, int64_t dil_w, int64_t groups,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/*
+ * Two chained quantized convs in one launch (ResNet56 stage-1 BasicBlock, reference
+ * models/resnet.py:55-71; each conv is QuantizedConv2d.forward, models/quantized_conv.py:
+ * 32-38): 3x3 / stride 1 / pad 1, 16 -> 16 -> 16 channels, x [N,16,H,W], w1 / w2 [16,16,3,3]
+ * quantized with the same (bits, fsr, mode):
+ *   y = act2(conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 (+ residual))
+ *   h = act1((conv(x, Q(w1)) + bias1) * post_scale1 + post_shift1)
+ * (every pointer but x, w1, w2, y may be NULL).  h never leaves the chip.  No workspace.
+ * po2q_qconv2d_pair_supported: 1 when this build has a plan for the shape (W % 4 == 0,
+ * W <= 224, C == 16, mode po2 / po2+, the exponent window inside bf16's range).
+ */
+int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
+int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, float* y,
+                          int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode,
+                          const float* bias1, const float* bias2,
+                          const float* post_scale1, const float* post_shift1, int act1,
+                          const float* post_scale2, const float* post_shift2, const float* residual, int act2,
+                          void* stream);
+
 typedef struct po2q_conv_plan po2q_conv_plan;
 int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index,
                              int64_t N, int64_t C, int64_t H, int64_t W,

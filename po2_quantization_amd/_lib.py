@@ -51,6 +51,8 @@ EXPORTS = (
     "po2q_qconv2d_plan_destroy",
     "po2q_qconv2d_wgrad_workspace_bytes",
     "po2q_qconv2d_wgrad_f32",
+    "po2q_qconv2d_pair_supported",
+    "po2q_qconv2d_pair_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -137,6 +139,8 @@ def load():
     L.po2q_qconv2d_f32_plan.argtypes = [i32, p, p, p, p] + [i64] * 14 + [i32, i32, i32, i32, p, sz, p]
     L.po2q_qconv2d_describe.restype = i32
     L.po2q_qconv2d_describe.argtypes = [i64] * 14 + [i32, i32, i32, i32, ctypes.c_char_p, sz]
+    L.po2q_qconv2d_pair_supported.restype = i32
+    L.po2q_qconv2d_pair_supported.argtypes = [i64] * 4 + [i32] * 3
     _lib = L
     return L
 
@@ -410,6 +414,31 @@ class SplitConv:
         _check(load().po2q_qconv2d_packed_f32(self._plan(), xc.data_ptr(), bp, y.data_ptr(), *self.key,
                                               self.ws.data_ptr(), self.ws.numel(), _stream(xc.device)))
         return y
+
+
+def pair_supported(x_shape, bits=4, mode="po2", fsr=1):
+    """True when qconv2d_pair has a kernel for this input shape (16 channels, W % 4 == 0,
+    W <= 224, po2 / po2+ with the exponent window inside bf16's range)."""
+    if mode not in ("po2", "po2+"):
+        return False
+    N, C, H, W = (int(v) for v in x_shape)
+    return bool(load().po2q_qconv2d_pair_supported(N, C, H, W, int(bits), int(fsr), MODES[mode]))
+
+
+def qconv2d_pair(x, w1, w2, bits=4, mode="po2", fsr=1, bias1=None, bias2=None, post_scale1=None, post_shift1=None,
+                 act1="none", post_scale2=None, post_shift2=None, residual=None, act2="none"):
+    """Two chained quantized 3x3 / stride-1 / pad-1 convs (16 -> 16 -> 16 channels) in one
+    launch (po2q_qconv2d_pair_f32), the intermediate kept on chip:
+        h = act1((conv(x, Q(w1)) + bias1) * post_scale1 + post_shift1)
+        y = act2((conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 + residual)
+    -- qconv2d_fused twice, as a ResNet56 stage-1 BasicBlock chains them (resnet.py:55-71)."""
+    for t, what in ((x, "input"), (w1, "weight1"), (w2, "weight2")):
+        _require_hip_f32(t, what)
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: qconv2d_pair needs the operator library (PO2Q_LIB selects another build)")
+    return _op_call(O.qconv2d_pair, x, w1, w2, int(bits), MODES[mode], int(fsr), bias1, bias2, post_scale1,
+                    post_shift1, ACTS[act1], post_scale2, post_shift2, residual, ACTS[act2])
 
 
 def conv_wgrad(x, gy, wshape, stride=1, padding=0, dilation=1, groups=1):

@@ -1,0 +1,538 @@
+// Two chained quantized 3x3 / stride-1 / pad-1 convs, C = 16 -> 16 -> 16, in ONE kernel:
+//   y = act2(Q(w2) * act1(Q(w1) * x  [* ps1 + pb1]) [* ps2 + pb2] (+ res))
+// -- the two QuantizedConv2d of a ResNet56 stage-1 BasicBlock (reference models/resnet.py:
+// 55-71; each conv is QuantizedConv2d.forward, models/quantized_conv.py:32-38) with the
+// block's eval BatchNorm / ReLU between and after them.  The intermediate activation never
+// goes to HBM: a block keeps it as a 2-row fp32 ring in LDS, so a pair moves x in + y out
+// (1.64 GB at bs = 256 @224) instead of twice that.
+//
+// Structure: the full-row-block kernel of po2q_conv_rowsf.hip (block = image x segment of
+// RB output rows x the whole width, 7 waves of 32 columns, one s_barrier per step, whole-row
+// LDS-DMA of x into a PD-slot raw ring, exact bf16x3 split into wave-private planes, row
+// reuse over the 3 tap rows, hand-counted vmcnt), run twice per step:
+//   step j:  wait for x row j (own DMAs), s_waitcnt lgkmcnt(0) + s_barrier, refill the slot
+//            of x row j-1 (+ the residual row of the output stored PD-1 steps later);
+//            conv 2 (j >= 3): split intermediate row j-3 from the shared ring (its halo
+//            columns are the neighbours' part), MFMAs with w2, output row j-5 -> epilogue
+//            2 -> transposed 128-byte-run stores;
+//            conv 1: split x row j, MFMAs with w1, intermediate row j-2 -> epilogue 1 ->
+//            the shared ring slot (j-2) & 1 (zeros outside the image: conv 2's padding).
+// A segment recomputes two intermediate rows of its neighbours (RB + 2 conv-1 rows).
+// Both weights are quantized + packed by the block itself (wq_* of po2q_quant_dev.h) into
+// VGPRs: one launch per pair, no pack kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <string>
+#include <type_traits>
+
+#include "../../include/po2q.h"
+#include "po2q_epi.h"
+#include "po2q_internal.h"
+#include "po2q_quant_dev.h"
+#include "po2q_rows_dev.h"
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+namespace {
+constexpr int kQSW = 32;                        // output columns per wave
+constexpr int kQPlane = (kQSW + 2) * 32 + 32;   // x planes (wave-private): [34 pixels][16 ch] bf16 + zero slot
+constexpr int kQResSlot = 64 * kQSW;            // residual of one wave's strip and row: [16][32] fp32
+}  // namespace
+
+struct PairArgs {
+    int N, H, W;      // P = H, Q = W
+    int Wp;           // 32 x waves
+    int YPL;          // bytes of one shared intermediate plane: (Wp + 3) pixels x 32 B
+    int RB, nseg, items, remap;
+    WQuant q1, q2;
+    const float* b1;  // conv biases (NULL: none)
+    const float* b2;
+    const float* ps1;  // epilogue 1 / 2: v * ps[k] + pb[k], then the activation (NULL parts skipped)
+    const float* pb1;
+    const float* ps2;
+    const float* pb2;
+    int act1, act2;
+    const float* res;  // RES: residual [N, 16, H, W] added before act2
+};
+
+// The intermediate h lives in LDS already split: 2 ring slots x 3 planes (hi / mid / lo)
+// x [Wp + 3 pixels][16 ch] bf16, pixel index = column + 1 (pixel 0 and Wp + 1 are conv 2's
+// zero padding columns, pixel Wp + 2 the zero slot of the k-step padding), shared by the
+// block: conv 2 reads its A fragments -- halo columns included -- straight from it.  Conv 1
+// runs in the transposed MFMA form (A = weights, B = x) so each lane holds 4 consecutive
+// channels of one pixel: its epilogue splits them and writes 8 contiguous bytes per plane.
+// PD: x ring slots.  NTS: non-temporal stores.  E: 0 = plain chain (no bias / affine /
+// activation / residual: y = scale * acc), 1 = the general epilogues (the kernel is bound
+// by vector-instruction issue, so the plain chain skips that work).
+template <int PD, int NTS, bool RES, int E = 1>
+__global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ x, float* __restrict__ y,
+                                                      PairArgs a) {
+    static_assert(PD >= 2 && PD <= 6, "raw ring slots");
+    constexpr int CC = 16, SW = kQSW, WC = SW + 2, PL = kQPlane, KS = 2, NG = SW / 16;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nw = (int)(blockDim.x >> 6);
+    const int rawslot = CC * a.Wp * 4;
+    const int yslot = 3 * a.YPL;
+    unsigned char* raw = lds;                                   // PD x [16][Wp] fp32 (x rows)
+    unsigned char* yr = raw + PD * rawslot;                     // 2 x 3 planes (intermediate, split)
+    unsigned char* slab = yr + 2 * yslot + wave * (3 * PL);     // this wave's x planes
+    unsigned char* resr = yr + 2 * yslot + nw * (3 * PL) + wave * (PD * kQResSlot);
+    const int zero_off = WC * CC * 2;
+    const int yzero = (a.Wp + 2) * 32;                          // zero slot of a shared plane
+
+    int blk = blockIdx.x;
+    if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
+    if (blk >= a.items) return;  // block-uniform
+    const int seg = blk % a.nseg;
+    const int n = blk / a.nseg;
+    const int p0 = seg * a.RB;
+    const int rbe = min(a.RB, a.H - p0);
+    const int nx = rbe + 4;      // x rows p0-2 .. p0+rbe+1
+    const int n1 = rbe + 2;      // intermediate rows p0-1 .. p0+rbe
+    const int nsteps = nx + 1;   // output row p0 + o completes at step o + 5
+    const int q0 = wave * SW;
+
+    // ---- x DMA: lane l of this wave's instruction i -> float4 e = 64(2w + i) + l of the
+    // row's 16 x Wp/4 float4 (whole-row runs; columns >= W read out of range: zeros)
+    const int HW = a.H * a.W;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
+    const int W4 = a.Wp >> 2;
+    uint32_t vi[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+        const int e = 64 * (NG * wave + i) + lane;
+        const int c = e / W4, q = 4 * (e - c * W4);
+        vi[i] = q < a.W ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
+    }
+    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    const __amdgpu_buffer_rsrc_t rres = rows_rsrc(RES ? a.res + (int64_t)n * CC * HW : x, RES ? CC * HW * 4 : 4);
+    uint32_t vr[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+        const int e = 64 * i + lane;
+        const int c = e / (SW / 4), q = q0 + 4 * (e % (SW / 4));
+        vr[i] = q < a.W ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
+    }
+    const uint32_t res_lds = (uint32_t)(uintptr_t)resr;
+    // x row jn into raw slot sl; with RES the residual of the output row stored at step jn
+    auto load_row = [&](int sl, int jn) __attribute__((always_inline)) {
+        const int h = p0 - 2 + jn;
+        const bool hok = jn < nx && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(NG * wave) * 1024u;
+#pragma unroll
+        for (int i = 0; i < NG; ++i)
+            rows_dma16<false>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
+        if constexpr (RES) {
+            const int o = jn - 5;
+            const bool ook = jn >= 5 && o < rbe;
+            const uint32_t ooff = (uint32_t)(ook ? p0 + o : 0) * (uint32_t)a.W * 4u;
+#pragma unroll
+            for (int i = 0; i < NG; ++i)
+                rows_dma16<false>(rres, (ook && vr[i] != 0x7fffffffu) ? vr[i] + ooff : 0x7fffffffu, 0u,
+                                  res_lds + (uint32_t)(sl * kQResSlot) + i * 1024u);
+        }
+    };
+
+    // ---- x split: lane -> (column sc of the strip, channel octet so); halo lanes < 32 ->
+    // (side, channel) from the neighbours' columns of the shared raw row (zero outside)
+    const int sc = lane % SW, so = lane / SW;
+    const int wa_i = x_addr<CC>(sc + 1, so);
+    const int hside = (lane / CC) & 1, hch = lane % CC;
+    const int hq = hside ? q0 + SW : q0 - 1;
+    const bool h_ok = lane < 2 * CC && hq >= 0 && hq < a.W;
+    const int wa_h = x_addr<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
+    const int rdx0 = (so * 8) * (a.Wp * 4) + (q0 + sc) * 4;
+    const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
+    // A / B fragment addresses: x planes (wave-private, pixel = strip column + 1) and the
+    // shared intermediate planes (pixel = column + 1)
+    int aoff[NG][KS], yoff[NG][KS];
+    {
+        const int p = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            aoff[grp][0] = x_addr<16>(16 * grp + p + (g >> 1), g & 1);
+            aoff[grp][1] = (g < 2) ? x_addr<16>(16 * grp + p + 2, g & 1) : zero_off;
+            yoff[grp][0] = x_addr<16>(q0 + 16 * grp + p + (g >> 1), g & 1);
+            yoff[grp][1] = (g < 2) ? x_addr<16>(q0 + 16 * grp + p + 2, g & 1) : yzero;
+        }
+    }
+
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * CC * HW, CC * HW * 4);
+    constexpr int ST = NG;                    // stores per step (issued every step; dropped ones out of range)
+    constexpr int LD = NG * (RES ? 2 : 1);    // DMAs per step
+    constexpr int VMW = ST + (PD - 2) * (LD + ST);
+
+    float scale1 = 1.0f, scale2 = 1.0f;
+    bool fin1 = true, fin2 = true;
+    bf16x8 bw1[3 * KS], bw2[3 * KS];
+    float bk1[E ? 4 : 1], e1s[E ? 4 : 1], e1b[E ? 4 : 1];  // conv 1: channels 4 (lane >> 4) + e
+    float bk2 = 0.0f, e2s = 1.0f, e2b = 0.0f;               // conv 2: channel lane & 15
+    floatx4 acc1[3][NG], acc2[3][NG];
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            acc1[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+            acc2[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    // 3 tap rows x 2 k-steps x 3 planes x NG groups of MFMAs on one split row (planes at
+    // `pb`, fragment offsets `off`) into accumulator slots SL; TR: transposed (A = weights)
+    auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG], const bf16x8 (&bw)[3 * KS], const unsigned char* pb,
+                     int pstride, const int (&off)[NG][KS]) __attribute__((always_inline)) {
+        constexpr int SR = decltype(S_)::value;
+        constexpr bool TR = decltype(TR_)::value;
+        constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 af[3][NG];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int grp = 0; grp < NG; ++grp)
+                    af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * pstride + off[grp][ks]));
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int grp = 0; grp < NG; ++grp)
+                        acc[SL[rr]][grp] =
+                            TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[rr * KS + ks], af[pl][grp], acc[SL[rr]][grp], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr * KS + ks], acc[SL[rr]][grp], 0, 0, 0);
+        }
+    };
+
+    auto step = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S6 = decltype(S_)::value;
+        constexpr int S = S6 % 3;
+        constexpr int D = (S + 2) % 3;          // the accumulator slot that completes
+        constexpr int YW = S6 & 1;              // ring slot written: intermediate row j-2
+        constexpr int YR = (S6 + 1) & 1;        // ring slot read: intermediate row j-3
+        const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
+        rows_wait<VMW>();  // this wave's part of x row j has landed
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + everyone's plane writes
+        load_row((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
+        // the x split's LDS reads next: their latency runs under conv 2's MFMAs
+        uint32_t bx[8], hx;
+        {
+            const unsigned char* rw = raw + RS * rawslot;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * (a.Wp * 4));
+            hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
+        }
+
+        // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
+        if (j >= 3) mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw2, yr + YR * yslot, a.YPL, yoff);
+        {
+            const int o = j - 5;
+            const bool orow = o >= 0 && o < rbe;
+            const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
+            const int ch = lane & 15, g = lane >> 4;
+            const uint32_t yrow = (uint32_t)ch * (uint32_t)HW + (uint32_t)(orow ? p0 + o : 0) * a.W;
+#pragma unroll
+            for (int grp = 0; grp < NG; ++grp) {
+                const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
+                floatx4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = E == 0 ? acc2[D][grp][e] * scale2 + 0.0f : (acc2[D][grp][e] * scale2 + bk2) * e2s + e2b;
+                if constexpr (RES) {
+                    const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += r[e];
+                }
+                if constexpr (E != 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
+                }
+                const int q = q0 + ql;
+                rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                acc2[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+
+        // ---- conv 1 on x row j (transposed MFMAs); intermediate row i = j - 2 completes
+        {
+            uint4 hi, mid, lo;
+            split3(bx, hi, mid, lo);
+            *reinterpret_cast<uint4*>(slab + wa_i) = hi;
+            *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
+            *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
+            if (lane < 2 * CC) {
+                uint16_t h16, m16, l16;
+                split1(h_ok ? hx : 0u, h16, m16, l16);
+                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+                *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
+                *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
+            }
+        }
+        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, slab, PL, aoff);
+        {
+            const int i = j - 2;
+            const int r1 = p0 - 1 + i;
+            const bool irow = i >= 0 && i < n1 && r1 >= 0 && r1 < a.H;
+            const int p = lane & 15, g = lane >> 4;
+            unsigned char* yw = yr + YW * yslot;
+#pragma unroll
+            for (int grp = 0; grp < NG; ++grp) {
+                // lane: pixel q0 + 16 grp + p, channels 4 g .. 4 g + 3
+                const int q = q0 + 16 * grp + p;
+                const bool ok = irow && q < a.W;
+                uint32_t b4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float t;
+                    if constexpr (E == 0) {
+                        t = acc1[D][grp][e] * scale1 + 0.0f;
+                    } else {
+                        t = epi_act((acc1[D][grp][e] * scale1 + bk1[e]) * e1s[e] + e1b[e], a.act1);
+                    }
+                    b4[e] = ok ? __float_as_uint(t) : 0u;
+                }
+                uint16_t h[4], m[4], l[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
+                const int wo = (q + 1) * 32 + 8 * g;
+                *reinterpret_cast<uint2*>(yw + wo) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+                *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
+                    make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+                *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
+                    make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+                acc1[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+
+    {
+        // x rows 0 .. PD-2, each followed by ST dropped stores (the steady-state count)
+        const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < PD - 1; ++r) {
+            load_row(r, r);
+#pragma unroll
+            for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
+        }
+    }
+    // ---- both weights quantized + packed into VGPRs while those DMAs fly (scratch: the
+    // intermediate planes, zeroed right after)
+    {
+        unsigned* red = reinterpret_cast<unsigned*>(yr);
+        unsigned* thr = red + 16;
+        scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
+#pragma unroll
+        for (int f = 0; f < 3 * KS; ++f)
+            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, 1, KS, f * 64 + lane, scale1, fin1, thr));
+        __syncthreads();  // red / thr reads of conv 1 done
+        scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
+#pragma unroll
+        for (int f = 0; f < 3 * KS; ++f)
+            bw2[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, 1, KS, f * 64 + lane, scale2, fin2, thr));
+        if constexpr (E != 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k1 = 4 * (lane >> 4) + e;
+                bk1[e] = a.b1 ? a.b1[k1] : 0.0f;
+                e1s[e] = a.ps1 ? a.ps1[k1] : 1.0f;
+                e1b[e] = a.pb1 ? a.pb1[k1] : 0.0f;
+            }
+            const int k2 = lane & 15;
+            bk2 = a.b2 ? a.b2[k2] : 0.0f;
+            e2s = a.ps2 ? a.ps2[k2] : 1.0f;
+            e2b = a.pb2 ? a.pb2[k2] : 0.0f;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every staged value lands here
+        if constexpr (E != 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(bk1[e]), "+v"(e1s[e]), "+v"(e1b[e]));
+            asm volatile("" : "+v"(bk2), "+v"(e2s), "+v"(e2b));
+        }
+#pragma unroll
+        for (int f = 0; f < 3 * KS; ++f) asm volatile("" : "+v"(bw1[f]), "+v"(bw2[f]));
+        __syncthreads();  // scratch reads done: zero the intermediate planes (padding columns, zero slots)
+        for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
+            reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
+        if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+        // step 0's barrier publishes the zeros
+    }
+    for (int j = 0; j < nsteps; j += 6) {
+        step(std::integral_constant<int, 0>{}, j);
+        step(std::integral_constant<int, 1>{}, j + 1);
+        step(std::integral_constant<int, 2>{}, j + 2);
+        if (j + 3 >= nsteps) break;
+        step(std::integral_constant<int, 3>{}, j + 3);
+        step(std::integral_constant<int, 4>{}, j + 4);
+        step(std::integral_constant<int, 5>{}, j + 5);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
+}
+
+// ------------------------------------------------------------------ planning --
+struct PairPlan {
+    int waves = 0, pd = 0, nts = 0, RB = 0, nseg = 0;
+    int64_t blocks = 0;
+    size_t lds = 0;
+};
+
+static size_t pair_lds(int waves, int pd, bool res) {
+    const int wp = kQSW * waves;
+    return (size_t)pd * 16 * wp * 4 + 2 * 3 * (size_t)(wp + 3) * 32 + (size_t)waves * 3 * kQPlane +
+           (res ? (size_t)waves * pd * kQResSlot : 0);
+}
+
+// One block per CU (7 waves at W = 224); segments of RB output rows: the fewest segments
+// that still give every CU a block, each recomputing 2 intermediate rows of its neighbours.
+static bool pair_plan(PairPlan& pp, int N, int H, int W, bool res, int pd, int nts) {
+    if (N <= 0 || H <= 0 || W <= 0 || W % 4 != 0) return false;
+    const int waves = (W + kQSW - 1) / kQSW;
+    if (waves > 7) return false;
+    if ((int64_t)16 * H * W * 4 >= (1LL << 31)) return false;
+    pp.waves = waves;
+    pp.pd = pd;
+    pp.nts = nts;
+    pp.lds = pair_lds(waves, pd, res);
+    if (pp.lds > 160 * 1024) return false;
+    int nseg = std::max(1, (256 + N - 1) / N);
+    nseg = std::min(nseg, std::max(1, H / 8));
+    pp.RB = (H + nseg - 1) / nseg;
+    pp.nseg = (H + pp.RB - 1) / pp.RB;
+    const int64_t items = (int64_t)N * pp.nseg;
+    if (items > INT_MAX / 2) return false;
+    pp.blocks = (items + 7) / 8 * 8;
+    return true;
+}
+
+template <int PD, int NTS>
+static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
+                                hipStream_t s) {
+    const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
+    const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
+    if (plain)
+        hipLaunchKernelGGL((conv_pair16<PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
+    else if (res)
+        hipLaunchKernelGGL((conv_pair16<PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
+    else
+        hipLaunchKernelGGL((conv_pair16<PD, NTS, false, 1>), grid, block, pp.lds, s, x, y, a);
+    return hipGetLastError();
+}
+
+static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
+                              hipStream_t s) {
+    if (pp.pd == 2 && pp.nts == 0) return launch_pair_t<2, 0>(pp, a, x, y, res, s);
+    if (pp.pd == 3 && pp.nts == 0) return launch_pair_t<3, 0>(pp, a, x, y, res, s);
+    if (pp.pd == 2 && pp.nts == 1) return launch_pair_t<2, 1>(pp, a, x, y, res, s);
+    if (pp.pd == 3 && pp.nts == 1) return launch_pair_t<3, 1>(pp, a, x, y, res, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace po2q
+
+// ------------------------------------------------------------------ C ABI --
+namespace {
+
+// variant knob: PO2Q_PAIR_VARIANT = pd * 10 + nts (pd 2 / 3 x ring slots, nts 0 / 1
+// non-temporal stores); default 20
+void pair_variant(int& pd, int& nts) {
+    pd = 2;
+    nts = 0;
+    if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
+        const int v = atoi(e);
+        const int d = v / 10, t = v % 10;
+        if ((d == 2 || d == 3) && (t == 0 || t == 1)) {
+            pd = d;
+            nts = t;
+        }
+    }
+}
+
+bool pair_args_ok(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode, int act1, int act2) {
+    if (N <= 0 || H <= 0 || W <= 0) {
+        po2q::set_error("po2q: pair: sizes must be positive");
+        return false;
+    }
+    if (C != 16) {
+        po2q::set_error("po2q: pair: 16 channels only (ResNet56 stage 1)");
+        return false;
+    }
+    if (mode != PO2Q_MODE_PO2 && mode != PO2Q_MODE_PO2_PLUS) {
+        po2q::set_error("po2q: pair: mode must be po2 or po2+");
+        return false;
+    }
+    if (bits < 1 || bits > 16) {
+        po2q::set_error("po2q: bits must be in [1, 16]");
+        return false;
+    }
+    const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
+    if (lo < -126 || hi > 127) {
+        po2q::set_error("po2q: pair: the exponent window leaves the bf16 range");
+        return false;
+    }
+    if (act1 < 0 || act1 > 3 || act2 < 0 || act2 > 3) {
+        po2q::set_error("po2q: unknown activation");
+        return false;
+    }
+    if (W % 4 != 0 || W > 224 || N * 16 * H * W >= (int64_t)INT32_MAX * 8) {
+        po2q::set_error("po2q: pair: W must be a multiple of 4 and at most 224");
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
+    po2q::PairPlan pp;
+    int pd, nts;
+    pair_variant(pd, nts);
+    return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) && po2q::pair_plan(pp, (int)N, (int)H, (int)W, true, pd, nts)
+               ? 1
+               : 0;
+}
+
+int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, float* y, int64_t N, int64_t C,
+                          int64_t H, int64_t W, int bits, int fsr, int mode, const float* bias1, const float* bias2,
+                          const float* post_scale1, const float* post_shift1, int act1, const float* post_scale2,
+                          const float* post_shift2, const float* residual, int act2, void* stream) {
+    if (!pair_args_ok(N, C, H, W, bits, fsr, mode, act1, act2)) return PO2Q_ERR_INVALID;
+    if (!x || !w1 || !w2 || !y) {
+        po2q::set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (residual == y || x == y) {
+        po2q::set_error("po2q: pair: y must not alias x or the residual");
+        return PO2Q_ERR_INVALID;
+    }
+    po2q::PairPlan pp;
+    int pd, nts;
+    pair_variant(pd, nts);
+    if (!po2q::pair_plan(pp, (int)N, (int)H, (int)W, residual != nullptr, pd, nts)) {
+        po2q::set_error("po2q: pair: no plan for this shape");
+        return PO2Q_ERR_UNSUPPORTED;
+    }
+    po2q::PairArgs a;
+    a.N = (int)N; a.H = (int)H; a.W = (int)W;
+    a.Wp = 32 * pp.waves;
+    a.YPL = (a.Wp + 3) * 32;
+    a.RB = pp.RB; a.nseg = pp.nseg; a.items = (int)(N * pp.nseg);
+    a.remap = (pp.blocks % 8 == 0) ? 1 : 0;
+    const int lo = fsr - (1 << (bits - 1)), hi = fsr - 1;
+    a.q1.w = w1; a.q1.n = 16 * 16 * 9; a.q1.lo = lo; a.q1.hi = hi; a.q1.mode = mode - 1;
+    a.q2 = a.q1;
+    a.q2.w = w2;
+    a.b1 = bias1; a.b2 = bias2;
+    a.ps1 = post_scale1; a.pb1 = post_shift1; a.act1 = act1;
+    a.ps2 = post_scale2; a.pb2 = post_shift2; a.act2 = act2;
+    a.res = residual;
+    const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));
+        return PO2Q_ERR_HIP;
+    }
+    return PO2Q_OK;
+}

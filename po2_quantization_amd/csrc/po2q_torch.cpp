@@ -10,6 +10,8 @@
 //                        (models/quantized_conv.py:32-38)
 //   po2q::qconv2d_fused  the same + eval BatchNorm affine, residual add and activation of
 //                        the blocks (resnet.py:55-71, mobilenet.py:32-33, mobile_vit.py:20-21)
+//   po2q::qconv2d_pair   two chained 16-channel 3x3 qconvs (+ BN / act between and after, residual)
+//                        in one launch: a ResNet56 stage-1 BasicBlock (resnet.py:55-71)
 //   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
 //                        STE, utils/quantizers.py:34-36)
 // Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
@@ -253,6 +255,62 @@ at::Tensor conv_wgrad(const at::Tensor& x_, const at::Tensor& dy_, at::IntArrayR
     return gw;
 }
 
+// Two chained 16-channel 3x3 convs in one launch (po2q_qconv2d_pair_f32)
+void check_vec(const c10::optional<at::Tensor>& t, const at::Tensor& x, int64_t n, const char* what) {
+    if (!t.has_value()) return;
+    check_hip_f32(*t, what);
+    TORCH_CHECK(t->device() == x.device(), "po2q: ", what, " must be on the input's device");
+    TORCH_CHECK(t->numel() == n, "po2q: ", what, " must have ", n, " elements, got ", t->numel());
+}
+
+at::Tensor qconv2d_pair(const at::Tensor& x_, const at::Tensor& w1_, const at::Tensor& w2_, int64_t bits, int64_t mode,
+                        int64_t fsr, const c10::optional<at::Tensor>& bias1, const c10::optional<at::Tensor>& bias2,
+                        const c10::optional<at::Tensor>& ps1, const c10::optional<at::Tensor>& pb1, int64_t act1,
+                        const c10::optional<at::Tensor>& ps2, const c10::optional<at::Tensor>& pb2,
+                        const c10::optional<at::Tensor>& residual, int64_t act2) {
+    check_hip_f32(x_, "input");
+    check_hip_f32(w1_, "weight1");
+    check_hip_f32(w2_, "weight2");
+    TORCH_CHECK(x_.dim() == 4 && w1_.dim() == 4 && w2_.dim() == 4, "po2q: pair: 4-D input and weights");
+    TORCH_CHECK(w1_.sizes() == w2_.sizes() && w1_.size(0) == x_.size(1) && w1_.size(1) == x_.size(1) &&
+                    w1_.size(2) == 3 && w1_.size(3) == 3,
+                "po2q: pair: weights must both be [C, C, 3, 3] with C = the input's channels");
+    TORCH_CHECK(w1_.device() == x_.device() && w2_.device() == x_.device(), "po2q: pair: tensors on one device");
+    const int64_t C = x_.size(1);
+    for (auto [t, what] : {std::make_pair(&bias1, "bias1"), std::make_pair(&bias2, "bias2"),
+                           std::make_pair(&ps1, "post_scale1"), std::make_pair(&pb1, "post_shift1"),
+                           std::make_pair(&ps2, "post_scale2"), std::make_pair(&pb2, "post_shift2")})
+        check_vec(*t, x_, C, what);
+    if (residual.has_value()) {
+        check_hip_f32(*residual, "residual");
+        TORCH_CHECK(residual->sizes() == x_.sizes() && residual->device() == x_.device(),
+                    "po2q: pair: residual must match the input's shape and device");
+    }
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous(), w1 = w1_.contiguous(), w2 = w2_.contiguous();
+    auto cont = [](const c10::optional<at::Tensor>& t) -> c10::optional<at::Tensor> {
+        return t.has_value() ? c10::optional<at::Tensor>(t->contiguous()) : c10::nullopt;
+    };
+    const auto b1c = cont(bias1), b2c = cont(bias2), s1 = cont(ps1), t1 = cont(pb1), s2 = cont(ps2), t2 = cont(pb2),
+               rc = cont(residual);
+    at::Tensor y = at::empty_like(x);
+    if (x.size(0) == 0) return y;
+    const int st = po2q_qconv2d_pair_f32(x.data_ptr<float>(), w1.data_ptr<float>(), w2.data_ptr<float>(),
+                                         y.data_ptr<float>(), x.size(0), C, x.size(2), x.size(3), (int)bits, (int)fsr,
+                                         (int)mode, opt_ptr(b1c), opt_ptr(b2c), opt_ptr(s1), opt_ptr(t1), (int)act1,
+                                         opt_ptr(s2), opt_ptr(t2), opt_ptr(rc), (int)act2, stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return y;
+}
+
+at::Tensor qconv2d_pair_meta(const at::Tensor& x, const at::Tensor&, const at::Tensor&, int64_t, int64_t, int64_t,
+                             const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
+                             const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, int64_t,
+                             const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
+                             const c10::optional<at::Tensor>&, int64_t) {
+    return at::empty_like(x);
+}
+
 // ---- Meta (shape-only) implementations ------------------------------------------
 at::Tensor qconv2d_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                         at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
@@ -292,6 +350,9 @@ TORCH_LIBRARY(po2q, m) {
           "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
     m.def("conv_wgrad(Tensor x, Tensor dy, int[] wshape, int[2] stride, int[2] padding, int[2] dilation, "
           "int groups=1) -> Tensor");
+    m.def("qconv2d_pair(Tensor x, Tensor w1, Tensor w2, int bits, int mode, int fsr=1, Tensor? bias1=None, "
+          "Tensor? bias2=None, Tensor? post_scale1=None, Tensor? post_shift1=None, int act1=0, "
+          "Tensor? post_scale2=None, Tensor? post_shift2=None, Tensor? residual=None, int act2=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
@@ -300,6 +361,7 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("qconv2d", &qconv2d);
     m.impl("qconv2d_fused", &qconv2d_fused);
     m.impl("conv_wgrad", &conv_wgrad);
+    m.impl("qconv2d_pair", &qconv2d_pair);
 }
 
 TORCH_LIBRARY_IMPL(po2q, Meta, m) {
@@ -308,4 +370,5 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("qconv2d", &qconv2d_meta);
     m.impl("qconv2d_fused", &qconv2d_fused_meta);
     m.impl("conv_wgrad", &conv_wgrad_meta);
+    m.impl("qconv2d_pair", &qconv2d_pair_meta);
 }

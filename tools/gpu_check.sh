@@ -37,6 +37,7 @@ for s in $STEPS; do
                    echo "stopping: conv GPU tests did not pass"; exit 1
                fi ;;
         bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        benchnp) run benchnp 600 python bench.py --steps 5 --warmup 2 --no-pair --no-cpu-baseline ;;
         models) run models_c2 300 python tools/model_bench.py --model resnet56 --image 32 --classes 10 --graph
                 run models_c3 300 python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --graph
                 run models_c5 300 python tools/model_bench.py --model mobilevit --image 256 --batch 64 --quantizer po2+ --bits 2 --graph
@@ -51,6 +52,11 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/dwtests.log || grep -q "failed\|error" gpurun_out/dwtests.log; then
                    echo "stopping: depthwise GPU tests did not pass"; exit 1
                fi ;;
+        pairtests) run pairtests 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/pairtests.log || grep -q "failed\|error" gpurun_out/pairtests.log; then
+                   echo "stopping: pair GPU tests did not pass"; exit 1
+               fi ;;
+        pairb) run pairb 300 python tools/pair_bench.py ;;
         dwb) run dwb 300 python tools/dw_bench.py ;;
         bwd) run bwd224 600 python tools/bwd_bench.py --batch 64
              run bwd32 600 python tools/bwd_bench.py --batch 256 --image 32
