@@ -417,8 +417,9 @@ class SplitConv:
 
 
 def pair_supported(x_shape, bits=4, mode="po2", fsr=1):
-    """True when qconv2d_pair has a kernel for this input shape (16 channels, W % 4 == 0,
-    W <= 224, po2 / po2+ with the exponent window inside bf16's range)."""
+    """True when qconv2d_pair takes this input shape (16 channels, W % 4 == 0, W <= 224,
+    po2 / po2+ with the exponent window inside bf16's range) and is the faster path (W >= 128;
+    below that two single-conv calls are faster)."""
     if mode not in ("po2", "po2+"):
         return False
     N, C, H, W = (int(v) for v in x_shape)

@@ -487,6 +487,9 @@ bool pair_args_ok(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr,
 }  // namespace
 
 int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
+    // below 4 waves per block (W < 128) a block is too narrow to hide its per-row latency:
+    // two single-conv launches are faster there (ResNet56 @32: 2.6 vs 2.0 ms per forward)
+    if (W < 128) return 0;
     po2q::PairPlan pp;
     int pd, nts;
     pair_variant(pd, nts);

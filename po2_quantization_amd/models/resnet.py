@@ -17,7 +17,9 @@ from typing import Callable, Optional
 import torch
 import torch.nn as nn
 
-from .quantized_conv import QuantizedConv2d, can_fuse, run_fused_sequence
+from .. import _lib
+from ..utils.quantizers import NATIVE_MODES
+from .quantized_conv import QuantizedConv2d, can_fuse, fold_bn, run_fused_sequence
 
 
 class BasicBlock(nn.Module):
@@ -37,6 +39,14 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         if can_fuse(self.bn1, self.bn2, self.downsample):
             # inference: conv+BN+ReLU and conv+BN+add+ReLU as single native calls
+            if self._pair_ok(x):
+                # conv1 -> bn1 -> relu -> conv2 -> bn2 -> + x -> relu as ONE launch, the
+                # intermediate kept on chip (po2q_qconv2d_pair_f32)
+                ps1, pb1 = fold_bn(self.bn1)
+                ps2, pb2 = fold_bn(self.bn2)
+                return _lib.qconv2d_pair(x, self.conv1.weight, self.conv2.weight, self.conv1.bits,
+                                         NATIVE_MODES[self.conv1.quantize_fn], post_scale1=ps1, post_shift1=pb1,
+                                         act1="relu", post_scale2=ps2, post_shift2=pb2, residual=x, act2="relu")
             shortcut = x if self.downsample is None else run_fused_sequence(self.downsample, x)
             out = self.conv1.fused(x, bn=self.bn1, act="relu")
             return self.conv2.fused(out, bn=self.bn2, residual=shortcut, act="relu")
@@ -45,6 +55,18 @@ class BasicBlock(nn.Module):
         out = self.bn2(self.conv2(out))
         out += shortcut
         return self.relu(out)
+
+    def _pair_ok(self, x):
+        """Both convs eligible for the pair kernel: identity shortcut, 16 channels, stride 1,
+        the same native PO2 quantizer and bits, bf16x3 arithmetic allowed."""
+        c1, c2 = self.conv1, self.conv2
+        mode = NATIVE_MODES.get(c1.quantize_fn)
+        return (self.downsample is None and mode in ("po2", "po2+") and c2.quantize_fn is c1.quantize_fn
+                and c1.bits == c2.bits and c1.in_channels == 16 and c1.out_channels == 16
+                and c2.out_channels == 16 and tuple(c1.stride) == (1, 1) and c1.precision != "fp32"
+                and c2.precision != "fp32" and c1.bias is None and c2.bias is None
+                and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and _lib.pair_supported(x.shape, c1.bits, mode))
 
     def get_quantization_error(self):
         e1, n1 = self.conv1.get_quantization_error()

@@ -102,6 +102,7 @@ def test_pair_rejects():
     x = torch.randn(1, 32, 8, 8, device=DEV)
     w = torch.randn(32, 32, 3, 3, device=DEV)
     assert not _lib.pair_supported(x.shape)
+    assert _lib.pair_supported((256, 16, 224, 224)) and not _lib.pair_supported((256, 16, 32, 32))
     with pytest.raises(_lib.Po2qError, match="16 channels"):
         _lib.qconv2d_pair(x, w, w)
     x = torch.randn(1, 16, 8, 10, device=DEV)

@@ -57,6 +57,10 @@ for s in $STEPS; do
                    echo "stopping: pair GPU tests did not pass"; exit 1
                fi ;;
         pairb) run pairb 300 python tools/pair_bench.py ;;
+        modeltests) run modeltests 600 python -u -m pytest tests/test_gpu_models.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/modeltests.log || grep -q "failed\|error" gpurun_out/modeltests.log; then
+                   echo "stopping: model GPU tests did not pass"; exit 1
+               fi ;;
         dwb) run dwb 300 python tools/dw_bench.py ;;
         bwd) run bwd224 600 python tools/bwd_bench.py --batch 64
              run bwd32 600 python tools/bwd_bench.py --batch 256 --image 32
