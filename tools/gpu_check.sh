@@ -92,6 +92,11 @@ for s in $STEPS; do
                      python3 tools/traffic.py gpurun_out/pmc_trows$i --algorithmic 1644185600 \
                          --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
                  done ;;
+        traffic_pair) run pmc_tpair 300 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" tpair "conv_pair16" hbm
+                 cp profiles/traffic.json gpurun_out/traffic.json
+                 python3 tools/traffic.py gpurun_out/pmc_tpair --algorithmic 1644274688 --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
+                 run pmc_pair 600 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" pair "conv_pair16" all
+                 python3 tools/pmc_summary.py gpurun_out/pmc_pair > gpurun_out/pmc_pair_summary.txt 2>&1 ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;
