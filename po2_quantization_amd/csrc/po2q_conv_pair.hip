@@ -152,15 +152,23 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
     const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
     // A / B fragment addresses: x planes (wave-private, pixel = strip column + 1) and the
     // shared intermediate planes (pixel = column + 1)
-    int aoff[NG][KS], yoff[NG][KS];
+    // shared planes: channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P at
+    // P * 32 + 8 * (c4 ^ ((P >> 2) & 3)) -- the 16 lanes of a ds_write_b64 group (16 pixels,
+    // one chunk) then cover all 32 banks; an A fragment (channel octet o) is the two chunks
+    // 2o, 2o + 1: two ds_read_b64 (yoff, yoff2)
+    auto ychunk = [](int P, int c4) { return P * 32 + 8 * (c4 ^ ((P >> 2) & 3)); };
+    int aoff[NG][KS], yoff[NG][KS], yoff2[NG][KS];
     {
         const int p = lane & 15, g = lane >> 4;
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp) {
             aoff[grp][0] = x_addr<16>(16 * grp + p + (g >> 1), g & 1);
             aoff[grp][1] = (g < 2) ? x_addr<16>(16 * grp + p + 2, g & 1) : zero_off;
-            yoff[grp][0] = x_addr<16>(q0 + 16 * grp + p + (g >> 1), g & 1);
-            yoff[grp][1] = (g < 2) ? x_addr<16>(q0 + 16 * grp + p + 2, g & 1) : yzero;
+            const int P0 = q0 + 16 * grp + p + (g >> 1), P1 = q0 + 16 * grp + p + 2, o = g & 1;
+            yoff[grp][0] = ychunk(P0, 2 * o);
+            yoff2[grp][0] = ychunk(P0, 2 * o + 1);
+            yoff[grp][1] = (g < 2) ? ychunk(P1, 2 * o) : yzero;
+            yoff2[grp][1] = (g < 2) ? ychunk(P1, 2 * o + 1) : yzero + 8;
         }
     }
 
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
     // 3 tap rows x 2 k-steps x 3 planes x NG groups of MFMAs on one split row (planes at
     // `pb`, fragment offsets `off`) into accumulator slots SL; TR: transposed (A = weights)
     auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG], const bf16x8 (&bw)[3 * KS], const unsigned char* pb,
-                     int pstride, const int (&off)[NG][KS]) __attribute__((always_inline)) {
+                     int pstride, const int (&off)[NG][KS], const int (&off2)[NG][KS]) __attribute__((always_inline)) {
         constexpr int SR = decltype(S_)::value;
         constexpr bool TR = decltype(TR_)::value;
         constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
@@ -196,7 +204,13 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
             for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                 for (int grp = 0; grp < NG; ++grp)
-                    af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * pstride + off[grp][ks]));
+                    if constexpr (TR) {  // x planes: one ds_read_b128
+                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * pstride + off[grp][ks]));
+                    } else {  // shared intermediate planes: two swizzled 8-byte chunks
+                        const uint2 u0 = *reinterpret_cast<const uint2*>(pb + pl * pstride + off[grp][ks]);
+                        const uint2 u1 = *reinterpret_cast<const uint2*>(pb + pl * pstride + off2[grp][ks]);
+                        af[pl][grp] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                    }
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
@@ -229,7 +243,8 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
         }
 
         // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
-        if (j >= 3) mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw2, yr + YR * yslot, a.YPL, yoff);
+        if (j >= 3)
+            mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw2, yr + YR * yslot, a.YPL, yoff, yoff2);
         {
             const int o = j - 5;
             const bool orow = o >= 0 && o < rbe;
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
                 *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
             }
         }
-        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, slab, PL, aoff);
+        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, slab, PL, aoff, aoff);
         {
             const int i = j - 2;
             const int r1 = p0 - 1 + i;
@@ -299,7 +314,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
                 uint16_t h[4], m[4], l[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
-                const int wo = (q + 1) * 32 + 8 * g;
+                const int wo = ychunk(q + 1, g);
                 *reinterpret_cast<uint2*>(yw + wo) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
                 *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
                     make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
