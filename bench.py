@@ -74,19 +74,19 @@ class QConvChain:
         self.mode, self.bits, self.precision = mode, bits, precision
         self.timed_layer = None      # index of the layer whose launches are timed
         self.events = []
-        self.pair = True             # conv1 -> conv2 of stage-1 blocks as one pair launch
+        self.pair = True             # conv1 -> conv2 of stage-1 / stage-2 blocks as one pair launch
 
     def conv(self, i, x):
         _, C, K, R, st, pad, _ = self.layers[i]
         return _lib.qconv2d(x, self.weights[i], None, st, pad, 1, 1, self.bits, self.mode, 1, self.precision)
 
     def pairable(self, i, x):
-        """conv1 -> conv2 of block i as ONE launch (po2q_qconv2d_pair_f32): both 3x3 s1 16->16."""
+        """conv1 -> conv2 of block i as ONE launch (po2q_qconv2d_pair_f32): both 3x3 s1 C->C, C = 16 / 32."""
         if not self.pair:
             return False
         (_, C1, K1, R1, s1, _, _), (_, C2, K2, R2, s2, _, _) = self.layers[i], self.layers[i + 1]
-        return (C1, K1, C2, K2, R1, R2, s1, s2) == (16, 16, 16, 16, 3, 3, 1, 1) and self.mode in ("po2", "po2+") \
-            and _lib.pair_supported(x.shape, self.bits, self.mode)
+        return C1 in (16, 32) and (K1, C2, K2, R1, R2, s1, s2) == (C1, C1, C1, 3, 3, 1, 1) \
+            and self.mode in ("po2", "po2+") and _lib.pair_supported(x.shape, self.bits, self.mode)
 
     def forward(self, x, record=False):
         i = 0
@@ -396,7 +396,7 @@ def main():
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
         "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
-                                  " (stage-1 conv1->conv2 pairs as one launch each)" if pair_used else "",
+                                  " (stage-1/2 conv1->conv2 pairs as one launch each)" if pair_used else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "conv_pairs": pair_used,
                    "autotune": _lib.benchmark,

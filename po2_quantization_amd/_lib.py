@@ -417,9 +417,9 @@ class SplitConv:
 
 
 def pair_supported(x_shape, bits=4, mode="po2", fsr=1):
-    """True when qconv2d_pair takes this input shape (16 channels, W % 4 == 0, W <= 224,
-    po2 / po2+ with the exponent window inside bf16's range) and is the faster path (W >= 128;
-    below that two single-conv calls are faster)."""
+    """True when qconv2d_pair takes this input shape (16 or 32 channels, W % 4 == 0, W <= 224
+    / 112, po2 / po2+ with the exponent window inside bf16's range) and is the faster path (at
+    least 4 waves per block: W >= 128 / 64; narrower rows: two single-conv calls)."""
     if mode not in ("po2", "po2+"):
         return False
     N, C, H, W = (int(v) for v in x_shape)
@@ -428,11 +428,11 @@ def pair_supported(x_shape, bits=4, mode="po2", fsr=1):
 
 def qconv2d_pair(x, w1, w2, bits=4, mode="po2", fsr=1, bias1=None, bias2=None, post_scale1=None, post_shift1=None,
                  act1="none", post_scale2=None, post_shift2=None, residual=None, act2="none"):
-    """Two chained quantized 3x3 / stride-1 / pad-1 convs (16 -> 16 -> 16 channels) in one
-    launch (po2q_qconv2d_pair_f32), the intermediate kept on chip:
+    """Two chained quantized 3x3 / stride-1 / pad-1 convs (C -> C -> C channels, C = 16 or 32)
+    in one launch (po2q_qconv2d_pair_f32), the intermediate kept on chip:
         h = act1((conv(x, Q(w1)) + bias1) * post_scale1 + post_shift1)
         y = act2((conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 + residual)
-    -- qconv2d_fused twice, as a ResNet56 stage-1 BasicBlock chains them (resnet.py:55-71)."""
+    -- qconv2d_fused twice, as a ResNet56 stage-1 / stage-2 BasicBlock chains them (resnet.py:55-71)."""
     for t, what in ((x, "input"), (w1, "weight1"), (w2, "weight2")):
         _require_hip_f32(t, what)
     O = ops()

@@ -38,15 +38,16 @@
 namespace po2q {
 
 namespace {
-constexpr int kQSW = 32;                        // output columns per wave
-constexpr int kQPlane = (kQSW + 2) * 32 + 32;   // x planes (wave-private): [34 pixels][16 ch] bf16 + zero slot
-constexpr int kQResSlot = 64 * kQSW;            // residual of one wave's strip and row: [16][32] fp32
+template <int CC> constexpr int kQSW = 512 / CC;                              // output columns per wave
+template <int CC> constexpr int kQPlane = (kQSW<CC> + 2) * 2 * CC + 32;      // x planes: [SW+2 px][CC] bf16 + zero slot
+constexpr int kQResSlot = 2048;                                               // residual of a wave's strip and row
+template <int CC> constexpr int kQKS = CC == 16 ? 2 : 3;                     // k-steps per tap row
 }  // namespace
 
 struct PairArgs {
     int N, H, W;      // P = H, Q = W
-    int Wp;           // 32 x waves
-    int YPL;          // bytes of one shared intermediate plane: (Wp + 3) pixels x 32 B
+    int Wp;           // SW x waves
+    int YPL;          // bytes of one shared intermediate plane: (Wp + 3) pixels x 2C bytes
     int RB, nseg, items, remap;
     WQuant q1, q2;
     const float* b1;  // conv biases (NULL: none)
@@ -56,35 +57,51 @@ struct PairArgs {
     const float* ps2;
     const float* pb2;
     int act1, act2;
-    const float* res;  // RES: residual [N, 16, H, W] added before act2
+    const float* res;  // RES: residual [N, C, H, W] added before act2
 };
 
+// Channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P in a shared intermediate
+// plane, XOR-swizzled so the 16 lanes of a ds_write_b64 group (16 pixels, one chunk) cover
+// all 32 banks of its 128-byte window.
+template <int CC>
+__device__ __forceinline__ int ychunk(int P, int c4) {
+    return P * (2 * CC) + 8 * (c4 ^ ((P >> (CC == 16 ? 2 : 1)) & (CC / 4 - 1)));
+}
+
 // The intermediate h lives in LDS already split: 2 ring slots x 3 planes (hi / mid / lo)
-// x [Wp + 3 pixels][16 ch] bf16, pixel index = column + 1 (pixel 0 and Wp + 1 are conv 2's
-// zero padding columns, pixel Wp + 2 the zero slot of the k-step padding), shared by the
-// block: conv 2 reads its A fragments -- halo columns included -- straight from it.  Conv 1
-// runs in the transposed MFMA form (A = weights, B = x) so each lane holds 4 consecutive
-// channels of one pixel: its epilogue splits them and writes 8 contiguous bytes per plane.
-// PD: x ring slots.  NTS: non-temporal stores.  E: 0 = plain chain (no bias / affine /
-// activation / residual: y = scale * acc), 1 = the general epilogues (the kernel is bound
-// by vector-instruction issue, so the plain chain skips that work).
-template <int PD, int NTS, bool RES, int E = 1>
-__global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ x, float* __restrict__ y,
-                                                      PairArgs a) {
+// x [Wp + 3 pixels][C ch] bf16, pixel index = column + 1 (pixel 0 and Wp + 1 are conv 2's
+// zero padding columns, pixel Wp + 2 the zero slot of C = 16's k-step padding), shared by
+// the block: conv 2 reads its A fragments -- halo columns included -- straight from it.
+// Conv 1 runs in the transposed MFMA form (A = weights, B = x) so each lane holds 4
+// consecutive channels of one pixel: its epilogue splits them and writes 8 bytes per plane.
+// CC: 16 (7 waves of 32 columns at W = 224, weights in VGPRs) or 32 (7 waves of 16 columns
+// at W = 112; conv 2's B fragments in LDS).  PD: x ring slots.  NTS: non-temporal stores.
+// E: 0 = plain chain (no bias / affine / activation / residual: y = scale * acc), 1 = the
+// general epilogues (the kernel is bound by vector-instruction issue, so the plain chain
+// skips that work).
+template <int CC, int PD, int NTS, bool RES, int E = 1>
+__global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
+                                                    PairArgs a) {
+    static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
-    constexpr int CC = 16, SW = kQSW, WC = SW + 2, PL = kQPlane, KS = 2, NG = SW / 16;
+    constexpr int SW = kQSW<CC>, WC = SW + 2, PL = kQPlane<CC>, KS = kQKS<CC>;
+    constexpr int NG = SW / 16;   // 16-pixel groups per wave
+    constexpr int NT = CC / 16;   // 16-channel output tiles (K = C)
+    constexpr int NF = 3 * KS * NT;                 // B fragments per conv
+    constexpr bool WL2 = CC == 32;                  // conv 2's B fragments in LDS (VGPR budget)
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nw = (int)(blockDim.x >> 6);
     const int rawslot = CC * a.Wp * 4;
     const int yslot = 3 * a.YPL;
-    unsigned char* raw = lds;                                   // PD x [16][Wp] fp32 (x rows)
+    unsigned char* raw = lds;                                   // PD x [C][Wp] fp32 (x rows)
     unsigned char* yr = raw + PD * rawslot;                     // 2 x 3 planes (intermediate, split)
     unsigned char* slab = yr + 2 * yslot + wave * (3 * PL);     // this wave's x planes
     unsigned char* resr = yr + 2 * yslot + nw * (3 * PL) + wave * (PD * kQResSlot);
+    uint4* wl2 = reinterpret_cast<uint4*>(yr + 2 * yslot + nw * (3 * PL) + (RES ? nw * PD * kQResSlot : 0));
     const int zero_off = WC * CC * 2;
-    const int yzero = (a.Wp + 2) * 32;                          // zero slot of a shared plane
+    const int yzero = (a.Wp + 2) * (2 * CC);                    // zero slot of a shared plane
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -99,22 +116,22 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
     const int q0 = wave * SW;
 
     // ---- x DMA: lane l of this wave's instruction i -> float4 e = 64(2w + i) + l of the
-    // row's 16 x Wp/4 float4 (whole-row runs; columns >= W read out of range: zeros)
+    // row's C x Wp/4 float4 (whole-row runs; columns >= W read out of range: zeros)
     const int HW = a.H * a.W;
     const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
     const int W4 = a.Wp >> 2;
-    uint32_t vi[NG];
+    uint32_t vi[2];
 #pragma unroll
-    for (int i = 0; i < NG; ++i) {
-        const int e = 64 * (NG * wave + i) + lane;
+    for (int i = 0; i < 2; ++i) {
+        const int e = 64 * (2 * wave + i) + lane;
         const int c = e / W4, q = 4 * (e - c * W4);
         vi[i] = q < a.W ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
     }
     const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
     const __amdgpu_buffer_rsrc_t rres = rows_rsrc(RES ? a.res + (int64_t)n * CC * HW : x, RES ? CC * HW * 4 : 4);
-    uint32_t vr[NG];
+    uint32_t vr[2];
 #pragma unroll
-    for (int i = 0; i < NG; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int e = 64 * i + lane;
         const int c = e / (SW / 4), q = q0 + 4 * (e % (SW / 4));
         vr[i] = q < a.W ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
@@ -125,22 +142,22 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
         const int h = p0 - 2 + jn;
         const bool hok = jn < nx && h >= 0 && h < a.H;
         const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
-        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(NG * wave) * 1024u;
+        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(2 * wave) * 1024u;
 #pragma unroll
-        for (int i = 0; i < NG; ++i)
+        for (int i = 0; i < 2; ++i)
             rows_dma16<false>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
         if constexpr (RES) {
             const int o = jn - 5;
             const bool ook = jn >= 5 && o < rbe;
             const uint32_t ooff = (uint32_t)(ook ? p0 + o : 0) * (uint32_t)a.W * 4u;
 #pragma unroll
-            for (int i = 0; i < NG; ++i)
+            for (int i = 0; i < 2; ++i)
                 rows_dma16<false>(rres, (ook && vr[i] != 0x7fffffffu) ? vr[i] + ooff : 0x7fffffffu, 0u,
                                   res_lds + (uint32_t)(sl * kQResSlot) + i * 1024u);
         }
     };
 
-    // ---- x split: lane -> (column sc of the strip, channel octet so); halo lanes < 32 ->
+    // ---- x split: lane -> (column sc of the strip, channel octet so); halo lanes < 2C ->
     // (side, channel) from the neighbours' columns of the shared raw row (zero outside)
     const int sc = lane % SW, so = lane / SW;
     const int wa_i = x_addr<CC>(sc + 1, so);
@@ -150,50 +167,61 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
     const int wa_h = x_addr<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
     const int rdx0 = (so * 8) * (a.Wp * 4) + (q0 + sc) * 4;
     const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
-    // A / B fragment addresses: x planes (wave-private, pixel = strip column + 1) and the
-    // shared intermediate planes (pixel = column + 1)
-    // shared planes: channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P at
-    // P * 32 + 8 * (c4 ^ ((P >> 2) & 3)) -- the 16 lanes of a ds_write_b64 group (16 pixels,
-    // one chunk) then cover all 32 banks; an A fragment (channel octet o) is the two chunks
-    // 2o, 2o + 1: two ds_read_b64 (yoff, yoff2)
-    auto ychunk = [](int P, int c4) { return P * 32 + 8 * (c4 ^ ((P >> 2) & 3)); };
+    // A fragment addresses: x planes (wave-private, pixel = strip column + 1): one b128;
+    // shared intermediate planes (pixel = column + 1): chunks 2o, 2o + 1 of the octet o, two b64
     int aoff[NG][KS], yoff[NG][KS], yoff2[NG][KS];
     {
         const int p = lane & 15, g = lane >> 4;
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp) {
-            aoff[grp][0] = x_addr<16>(16 * grp + p + (g >> 1), g & 1);
-            aoff[grp][1] = (g < 2) ? x_addr<16>(16 * grp + p + 2, g & 1) : zero_off;
-            const int P0 = q0 + 16 * grp + p + (g >> 1), P1 = q0 + 16 * grp + p + 2, o = g & 1;
-            yoff[grp][0] = ychunk(P0, 2 * o);
-            yoff2[grp][0] = ychunk(P0, 2 * o + 1);
-            yoff[grp][1] = (g < 2) ? ychunk(P1, 2 * o) : yzero;
-            yoff2[grp][1] = (g < 2) ? ychunk(P1, 2 * o + 1) : yzero + 8;
+            const int qc = q0 + 16 * grp + p;  // output column
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                int xp, yp, o;
+                bool zero;
+                if constexpr (CC == 16) {  // ks 0: taps (s0 | s1) x 16 ch; ks 1: (s2 | zero)
+                    xp = 16 * grp + p + (ks == 0 ? (g >> 1) : 2);
+                    yp = qc + (ks == 0 ? (g >> 1) : 2);
+                    o = g & 1;
+                    zero = ks == 1 && g >= 2;
+                } else {  // ks = tap s, k = the 32 channels (octet g)
+                    xp = 16 * grp + p + ks;
+                    yp = qc + ks;
+                    o = g;
+                    zero = false;
+                }
+                aoff[grp][ks] = zero ? zero_off : x_addr<CC>(xp, o);
+                yoff[grp][ks] = zero ? yzero : ychunk<CC>(yp, 2 * o);
+                yoff2[grp][ks] = zero ? yzero + 8 : ychunk<CC>(yp, 2 * o + 1);
+            }
         }
     }
 
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * CC * HW, CC * HW * 4);
-    constexpr int ST = NG;                    // stores per step (issued every step; dropped ones out of range)
-    constexpr int LD = NG * (RES ? 2 : 1);    // DMAs per step
+    constexpr int ST = NG * NT;               // stores per step (issued every step; dropped ones out of range)
+    constexpr int LD = RES ? 4 : 2;           // DMAs per step
     constexpr int VMW = ST + (PD - 2) * (LD + ST);
 
     float scale1 = 1.0f, scale2 = 1.0f;
     bool fin1 = true, fin2 = true;
-    bf16x8 bw1[3 * KS], bw2[3 * KS];
-    float bk1[E ? 4 : 1], e1s[E ? 4 : 1], e1b[E ? 4 : 1];  // conv 1: channels 4 (lane >> 4) + e
-    float bk2 = 0.0f, e2s = 1.0f, e2b = 0.0f;               // conv 2: channel lane & 15
-    floatx4 acc1[3][NG], acc2[3][NG];
+    bf16x8 bw1[NF], bw2[WL2 ? 1 : NF];
+    float bk1[E ? NT * 4 : 1], e1s[E ? NT * 4 : 1], e1b[E ? NT * 4 : 1];  // conv 1: ch 16 nt + 4 (lane >> 4) + e
+    float bk2[NT], e2s[NT], e2b[NT];                                       // conv 2: ch 16 nt + (lane & 15)
+    floatx4 acc1[3][NG][NT], acc2[3][NG][NT];
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl)
 #pragma unroll
-        for (int grp = 0; grp < NG; ++grp) {
-            acc1[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
-            acc2[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-    // 3 tap rows x 2 k-steps x 3 planes x NG groups of MFMAs on one split row (planes at
-    // `pb`, fragment offsets `off`) into accumulator slots SL; TR: transposed (A = weights)
-    auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG], const bf16x8 (&bw)[3 * KS], const unsigned char* pb,
-                     int pstride, const int (&off)[NG][KS], const int (&off2)[NG][KS]) __attribute__((always_inline)) {
+        for (int grp = 0; grp < NG; ++grp)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                acc1[sl][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+                acc2[sl][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+    // 3 tap rows x KS k-steps x 3 planes x NG groups x NT tiles of MFMAs on one split row
+    // into accumulator slots SL.  TR (conv 1): transposed (A = weights), x planes, VGPR
+    // weights; else (conv 2): shared planes (two b64 per fragment), weights per WL2
+    auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG][NT], const bf16x8 (&bw)[NF],
+                     const bf16x8 (&bw2v)[WL2 ? 1 : NF], const unsigned char* pb) __attribute__((always_inline)) {
         constexpr int SR = decltype(S_)::value;
         constexpr bool TR = decltype(TR_)::value;
         constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
@@ -203,23 +231,35 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-                for (int grp = 0; grp < NG; ++grp)
-                    if constexpr (TR) {  // x planes: one ds_read_b128
-                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * pstride + off[grp][ks]));
-                    } else {  // shared intermediate planes: two swizzled 8-byte chunks
-                        const uint2 u0 = *reinterpret_cast<const uint2*>(pb + pl * pstride + off[grp][ks]);
-                        const uint2 u1 = *reinterpret_cast<const uint2*>(pb + pl * pstride + off2[grp][ks]);
+                for (int grp = 0; grp < NG; ++grp) {
+                    if constexpr (TR) {
+                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
+                    } else {
+                        const uint2 u0 = *reinterpret_cast<const uint2*>(pb + pl * a.YPL + yoff[grp][ks]);
+                        const uint2 u1 = *reinterpret_cast<const uint2*>(pb + pl * a.YPL + yoff2[grp][ks]);
                         af[pl][grp] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
                     }
+                }
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int f = (rr * KS + ks) * NT + nt;
+                    bf16x8 b;
+                    if constexpr (TR)
+                        b = bw[f];
+                    else if constexpr (WL2)
+                        b = __builtin_bit_cast(bf16x8, wl2[f * 64 + lane]);
+                    else
+                        b = bw2v[WL2 ? 0 : f];
 #pragma unroll
-                    for (int grp = 0; grp < NG; ++grp)
-                        acc[SL[rr]][grp] =
-                            TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[rr * KS + ks], af[pl][grp], acc[SL[rr]][grp], 0, 0, 0)
-                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr * KS + ks], acc[SL[rr]][grp], 0, 0, 0);
+                    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                        for (int grp = 0; grp < NG; ++grp)
+                            acc[SL[rr]][grp][nt] =
+                                TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], acc[SL[rr]][grp][nt], 0, 0, 0)
+                                   : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, acc[SL[rr]][grp][nt], 0, 0, 0);
+                }
         }
     };
 
@@ -243,33 +283,37 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
         }
 
         // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
-        if (j >= 3)
-            mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw2, yr + YR * yslot, a.YPL, yoff, yoff2);
+        if (j >= 3) mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
         {
             const int o = j - 5;
             const bool orow = o >= 0 && o < rbe;
             const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
-            const int ch = lane & 15, g = lane >> 4;
-            const uint32_t yrow = (uint32_t)ch * (uint32_t)HW + (uint32_t)(orow ? p0 + o : 0) * a.W;
+            const int g = lane >> 4;
 #pragma unroll
-            for (int grp = 0; grp < NG; ++grp) {
-                const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
-                floatx4 v;
+            for (int nt = 0; nt < NT; ++nt) {
+                const int ch = 16 * nt + (lane & 15);
+                const uint32_t yrow = (uint32_t)ch * (uint32_t)HW + (uint32_t)(orow ? p0 + o : 0) * a.W;
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    v[e] = E == 0 ? acc2[D][grp][e] * scale2 + 0.0f : (acc2[D][grp][e] * scale2 + bk2) * e2s + e2b;
-                if constexpr (RES) {
-                    const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
+                for (int grp = 0; grp < NG; ++grp) {
+                    const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
+                    floatx4 v;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] += r[e];
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
+                                      : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                    if constexpr (RES) {
+                        const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] += r[e];
+                    }
+                    if constexpr (E != 0) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
+                    }
+                    const int q = q0 + ql;
+                    rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    acc2[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
                 }
-                if constexpr (E != 0) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
-                }
-                const int q = q0 + ql;
-                rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
-                acc2[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
 
@@ -288,7 +332,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
                 *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
             }
         }
-        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, slab, PL, aoff, aoff);
+        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, bw2, slab);
         {
             const int i = j - 2;
             const int r1 = p0 - 1 + i;
@@ -297,30 +341,34 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
             unsigned char* yw = yr + YW * yslot;
 #pragma unroll
             for (int grp = 0; grp < NG; ++grp) {
-                // lane: pixel q0 + 16 grp + p, channels 4 g .. 4 g + 3
-                const int q = q0 + 16 * grp + p;
+                const int q = q0 + 16 * grp + p;  // lane: pixel q, channels 16 nt + 4 g .. + 3
                 const bool ok = irow && q < a.W;
-                uint32_t b4[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float t;
-                    if constexpr (E == 0) {
-                        t = acc1[D][grp][e] * scale1 + 0.0f;
-                    } else {
-                        t = epi_act((acc1[D][grp][e] * scale1 + bk1[e]) * e1s[e] + e1b[e], a.act1);
+                for (int nt = 0; nt < NT; ++nt) {
+                    uint32_t b4[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float t;
+                        if constexpr (E == 0) {
+                            t = acc1[D][grp][nt][e] * scale1 + 0.0f;
+                        } else {
+                            const int c = nt * 4 + e;
+                            t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
+                        }
+                        b4[e] = ok ? __float_as_uint(t) : 0u;
                     }
-                    b4[e] = ok ? __float_as_uint(t) : 0u;
-                }
-                uint16_t h[4], m[4], l[4];
+                    uint16_t h[4], m[4], l[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
-                const int wo = ychunk(q + 1, g);
-                *reinterpret_cast<uint2*>(yw + wo) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-                *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
-                    make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
-                *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
-                    make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
-                acc1[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+                    for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
+                    const int wo = ychunk<CC>(q + 1, 4 * nt + g);
+                    *reinterpret_cast<uint2*>(yw + wo) =
+                        make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+                    *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
+                        make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+                    *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
+                        make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+                    acc1[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
             }
         }
     };
@@ -335,46 +383,61 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
             for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
         }
     }
-    // ---- both weights quantized + packed into VGPRs while those DMAs fly (scratch: the
-    // intermediate planes, zeroed right after)
+    // ---- both weights quantized + packed (VGPRs; conv 2's in LDS for C = 32) while those
+    // DMAs fly (scratch: the intermediate planes, zeroed right after)
     {
         unsigned* red = reinterpret_cast<unsigned*>(yr);
         unsigned* thr = red + 16;
         scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
 #pragma unroll
-        for (int f = 0; f < 3 * KS; ++f)
-            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, 1, KS, f * 64 + lane, scale1, fin1, thr));
+        for (int f = 0; f < NF; ++f)
+            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr));
         __syncthreads();  // red / thr reads of conv 1 done
         scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
+        if constexpr (WL2) {
+            for (int e = tid; e < NF * 64; e += blockDim.x) wl2[e] = wq_frag_rows(a.q2, CC, CC, CC, NT, KS, e, scale2, fin2, thr);
+        } else {
 #pragma unroll
-        for (int f = 0; f < 3 * KS; ++f)
-            bw2[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, 1, KS, f * 64 + lane, scale2, fin2, thr));
-        if constexpr (E != 0) {
+            for (int f = 0; f < NF; ++f)
+                bw2[WL2 ? 0 : f] =
+                    __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
+        }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k1 = 4 * (lane >> 4) + e;
-                bk1[e] = a.b1 ? a.b1[k1] : 0.0f;
-                e1s[e] = a.ps1 ? a.ps1[k1] : 1.0f;
-                e1b[e] = a.pb1 ? a.pb1[k1] : 0.0f;
+        for (int nt = 0; nt < NT; ++nt) {
+            if constexpr (E != 0) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k1 = 16 * nt + 4 * (lane >> 4) + e;
+                    bk1[nt * 4 + e] = a.b1 ? a.b1[k1] : 0.0f;
+                    e1s[nt * 4 + e] = a.ps1 ? a.ps1[k1] : 1.0f;
+                    e1b[nt * 4 + e] = a.pb1 ? a.pb1[k1] : 0.0f;
+                }
             }
-            const int k2 = lane & 15;
-            bk2 = a.b2 ? a.b2[k2] : 0.0f;
-            e2s = a.ps2 ? a.ps2[k2] : 1.0f;
-            e2b = a.pb2 ? a.pb2[k2] : 0.0f;
+            const int k2 = 16 * nt + (lane & 15);
+            bk2[nt] = (E && a.b2) ? a.b2[k2] : 0.0f;
+            e2s[nt] = (E && a.ps2) ? a.ps2[k2] : 1.0f;
+            e2b[nt] = (E && a.pb2) ? a.pb2[k2] : 0.0f;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every staged value lands here
-        if constexpr (E != 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(bk1[e]), "+v"(e1s[e]), "+v"(e1b[e]));
-            asm volatile("" : "+v"(bk2), "+v"(e2s), "+v"(e2b));
+        for (int nt = 0; nt < NT; ++nt) {
+            if constexpr (E != 0) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(bk1[nt * 4 + e]), "+v"(e1s[nt * 4 + e]), "+v"(e1b[nt * 4 + e]));
+            }
+            asm volatile("" : "+v"(bk2[nt]), "+v"(e2s[nt]), "+v"(e2b[nt]));
         }
 #pragma unroll
-        for (int f = 0; f < 3 * KS; ++f) asm volatile("" : "+v"(bw1[f]), "+v"(bw2[f]));
+        for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw1[f]));
+        if constexpr (!WL2) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw2[WL2 ? 0 : f]));
+        }
         __syncthreads();  // scratch reads done: zero the intermediate planes (padding columns, zero slots)
         for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
             reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
         if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
-        // step 0's barrier publishes the zeros
+        // step 0's barrier publishes the zeros (and wl2)
     }
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
@@ -390,28 +453,32 @@ __global__ __launch_bounds__(448, 1) void conv_pair16(const float* __restrict__ 
 
 // ------------------------------------------------------------------ planning --
 struct PairPlan {
-    int waves = 0, pd = 0, nts = 0, RB = 0, nseg = 0;
+    int C = 0, waves = 0, pd = 0, nts = 0, RB = 0, nseg = 0;
     int64_t blocks = 0;
     size_t lds = 0;
 };
 
-static size_t pair_lds(int waves, int pd, bool res) {
-    const int wp = kQSW * waves;
-    return (size_t)pd * 16 * wp * 4 + 2 * 3 * (size_t)(wp + 3) * 32 + (size_t)waves * 3 * kQPlane +
-           (res ? (size_t)waves * pd * kQResSlot : 0);
+static size_t pair_lds(int C, int waves, int pd, bool res) {
+    const int sw = 512 / C, wp = sw * waves;
+    const int plane = (sw + 2) * 2 * C + 32;
+    const int nf = 3 * (C == 16 ? 2 : 3) * (C / 16);
+    return (size_t)pd * C * wp * 4 + 2 * 3 * (size_t)(wp + 3) * 2 * C + (size_t)waves * 3 * plane +
+           (res ? (size_t)waves * pd * kQResSlot : 0) + (C == 32 ? (size_t)nf * 64 * 16 : 0);
 }
 
-// One block per CU (7 waves at W = 224); segments of RB output rows: the fewest segments
-// that still give every CU a block, each recomputing 2 intermediate rows of its neighbours.
-static bool pair_plan(PairPlan& pp, int N, int H, int W, bool res, int pd, int nts) {
-    if (N <= 0 || H <= 0 || W <= 0 || W % 4 != 0) return false;
-    const int waves = (W + kQSW - 1) / kQSW;
+// One block per CU (7 waves); segments of RB output rows: the fewest segments that still
+// give every CU a block, each recomputing 2 intermediate rows of its neighbours.
+static bool pair_plan(PairPlan& pp, int N, int C, int H, int W, bool res, int pd, int nts) {
+    if (N <= 0 || H <= 0 || W <= 0 || W % 4 != 0 || (C != 16 && C != 32)) return false;
+    const int sw = 512 / C;
+    const int waves = (W + sw - 1) / sw;
     if (waves > 7) return false;
-    if ((int64_t)16 * H * W * 4 >= (1LL << 31)) return false;
+    if ((int64_t)C * H * W * 4 >= (1LL << 31)) return false;
+    pp.C = C;
     pp.waves = waves;
     pp.pd = pd;
     pp.nts = nts;
-    pp.lds = pair_lds(waves, pd, res);
+    pp.lds = pair_lds(C, waves, pd, res);
     if (pp.lds > 160 * 1024) return false;
     int nseg = std::max(1, (256 + N - 1) / N);
     nseg = std::min(nseg, std::max(1, H / 8));
@@ -423,26 +490,27 @@ static bool pair_plan(PairPlan& pp, int N, int H, int W, bool res, int pd, int n
     return true;
 }
 
-template <int PD, int NTS>
+template <int CC, int PD, int NTS>
 static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
                                 hipStream_t s) {
     const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
     const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
     if (plain)
-        hipLaunchKernelGGL((conv_pair16<PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
     else if (res)
-        hipLaunchKernelGGL((conv_pair16<PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
     else
-        hipLaunchKernelGGL((conv_pair16<PD, NTS, false, 1>), grid, block, pp.lds, s, x, y, a);
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1>), grid, block, pp.lds, s, x, y, a);
     return hipGetLastError();
 }
 
 static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
                               hipStream_t s) {
-    if (pp.pd == 2 && pp.nts == 0) return launch_pair_t<2, 0>(pp, a, x, y, res, s);
-    if (pp.pd == 3 && pp.nts == 0) return launch_pair_t<3, 0>(pp, a, x, y, res, s);
-    if (pp.pd == 2 && pp.nts == 1) return launch_pair_t<2, 1>(pp, a, x, y, res, s);
-    if (pp.pd == 3 && pp.nts == 1) return launch_pair_t<3, 1>(pp, a, x, y, res, s);
+#define PO2Q_PR(c, d, nt) \
+    if (pp.C == c && pp.pd == d && pp.nts == nt) return launch_pair_t<c, d, nt>(pp, a, x, y, res, s);
+    PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
+    PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
+#undef PO2Q_PR
     return hipErrorInvalidValue;
 }
 
@@ -471,8 +539,8 @@ bool pair_args_ok(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr,
         po2q::set_error("po2q: pair: sizes must be positive");
         return false;
     }
-    if (C != 16) {
-        po2q::set_error("po2q: pair: 16 channels only (ResNet56 stage 1)");
+    if (C != 16 && C != 32) {
+        po2q::set_error("po2q: pair: 16 or 32 channels only (ResNet56 stages 1 and 2)");
         return false;
     }
     if (mode != PO2Q_MODE_PO2 && mode != PO2Q_MODE_PO2_PLUS) {
@@ -492,8 +560,8 @@ bool pair_args_ok(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr,
         po2q::set_error("po2q: unknown activation");
         return false;
     }
-    if (W % 4 != 0 || W > 224 || N * 16 * H * W >= (int64_t)INT32_MAX * 8) {
-        po2q::set_error("po2q: pair: W must be a multiple of 4 and at most 224");
+    if (W % 4 != 0 || W > 7 * (512 / C)) {
+        po2q::set_error("po2q: pair: W must be a multiple of 4 and at most 7 x 512 / C (224 for C = 16, 112 for 32)");
         return false;
     }
     return true;
@@ -502,13 +570,14 @@ bool pair_args_ok(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr,
 }  // namespace
 
 int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
-    // below 4 waves per block (W < 128) a block is too narrow to hide its per-row latency:
-    // two single-conv launches are faster there (ResNet56 @32: 2.6 vs 2.0 ms per forward)
-    if (W < 128) return 0;
+    // below 4 waves per block a block is too narrow to hide its per-row latency: two
+    // single-conv launches are faster there (ResNet56 @32: 2.6 vs 2.0 ms per forward)
+    if ((C == 16 || C == 32) && W <= 3 * (512 / C)) return 0;
     po2q::PairPlan pp;
     int pd, nts;
     pair_variant(pd, nts);
-    return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) && po2q::pair_plan(pp, (int)N, (int)H, (int)W, true, pd, nts)
+    return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) &&
+                   po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, true, pd, nts)
                ? 1
                : 0;
 }
@@ -529,18 +598,18 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     po2q::PairPlan pp;
     int pd, nts;
     pair_variant(pd, nts);
-    if (!po2q::pair_plan(pp, (int)N, (int)H, (int)W, residual != nullptr, pd, nts)) {
+    if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, residual != nullptr, pd, nts)) {
         po2q::set_error("po2q: pair: no plan for this shape");
         return PO2Q_ERR_UNSUPPORTED;
     }
     po2q::PairArgs a;
     a.N = (int)N; a.H = (int)H; a.W = (int)W;
-    a.Wp = 32 * pp.waves;
-    a.YPL = (a.Wp + 3) * 32;
+    a.Wp = (512 / (int)C) * pp.waves;
+    a.YPL = (a.Wp + 3) * 2 * (int)C;
     a.RB = pp.RB; a.nseg = pp.nseg; a.items = (int)(N * pp.nseg);
     a.remap = (pp.blocks % 8 == 0) ? 1 : 0;
     const int lo = fsr - (1 << (bits - 1)), hi = fsr - 1;
-    a.q1.w = w1; a.q1.n = 16 * 16 * 9; a.q1.lo = lo; a.q1.hi = hi; a.q1.mode = mode - 1;
+    a.q1.w = w1; a.q1.n = (int)(C * C * 9); a.q1.lo = lo; a.q1.hi = hi; a.q1.mode = mode - 1;
     a.q2 = a.q1;
     a.q2.w = w2;
     a.b1 = bias1; a.b2 = bias2;

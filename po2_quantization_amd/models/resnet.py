@@ -57,13 +57,13 @@ class BasicBlock(nn.Module):
         return self.relu(out)
 
     def _pair_ok(self, x):
-        """Both convs eligible for the pair kernel: identity shortcut, 16 channels, stride 1,
+        """Both convs eligible for the pair kernel: identity shortcut, 16 or 32 channels, stride 1,
         the same native PO2 quantizer and bits, bf16x3 arithmetic allowed."""
         c1, c2 = self.conv1, self.conv2
         mode = NATIVE_MODES.get(c1.quantize_fn)
         return (self.downsample is None and mode in ("po2", "po2+") and c2.quantize_fn is c1.quantize_fn
-                and c1.bits == c2.bits and c1.in_channels == 16 and c1.out_channels == 16
-                and c2.out_channels == 16 and tuple(c1.stride) == (1, 1) and c1.precision != "fp32"
+                and c1.bits == c2.bits and c1.in_channels in (16, 32) and c1.out_channels == c1.in_channels
+                and c2.out_channels == c1.in_channels and tuple(c1.stride) == (1, 1) and c1.precision != "fp32"
                 and c2.precision != "fp32" and c1.bias is None and c2.bias is None
                 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
                 and _lib.pair_supported(x.shape, c1.bits, mode))

@@ -19,17 +19,17 @@ def nerr(y, ref):
     return ((y - ref).abs().max() / ref.abs().max()).item()
 
 
-def make(N, H, W, seed, affine):
+def make(N, H, W, seed, affine, C=16):
     g = torch.Generator().manual_seed(seed)
-    x = torch.randn(N, 16, H, W, generator=g).to(DEV)
-    w1 = (torch.randn(16, 16, 3, 3, generator=g) * 0.12).to(DEV)
-    w2 = (torch.randn(16, 16, 3, 3, generator=g) * 0.12).to(DEV)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    w1 = (torch.randn(C, C, 3, 3, generator=g) * 0.12).to(DEV)
+    w2 = (torch.randn(C, C, 3, 3, generator=g) * 0.12).to(DEV)
     e = {}
     if affine:
         for k in ("post_scale1", "post_scale2"):
-            e[k] = (torch.rand(16, generator=g) + 0.5).to(DEV)
+            e[k] = (torch.rand(C, generator=g) + 0.5).to(DEV)
         for k in ("post_shift1", "post_shift2"):
-            e[k] = (torch.randn(16, generator=g) * 0.1).to(DEV)
+            e[k] = (torch.randn(C, generator=g) * 0.1).to(DEV)
     return x, w1, w2, e
 
 
@@ -47,38 +47,42 @@ def torch_chain(x, w1, w2, e, act1, act2, res, mode="po2", bias1=None, bias2=Non
     return ACT[act2](y)
 
 
-SHAPES = [(2, 20, 32), (1, 9, 224), (3, 37, 68), (2, 1, 36), (1, 2, 8), (2, 56, 56), (4, 17, 224)]
+SHAPES = [(2, 20, 32, 16), (1, 9, 224, 16), (3, 37, 68, 16), (2, 1, 36, 16), (1, 2, 8, 16), (2, 56, 56, 16),
+          (4, 17, 224, 16),
+          (2, 20, 32, 32), (1, 9, 112, 32), (3, 37, 68, 32), (2, 1, 36, 32), (1, 2, 8, 32), (4, 13, 112, 32)]
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 @pytest.mark.parametrize("variant", ["20", "30", "21", "31"])
 def test_pair_chain_vs_torch(shape, variant, monkeypatch):
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", variant)
-    N, H, W = shape
-    x, w1, w2, _ = make(N, H, W, hash(shape) & 0xFFFF, False)
+    N, H, W, C = shape
+    x, w1, w2, _ = make(N, H, W, hash(shape) & 0xFFFF, False, C)
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
     ref = torch_chain(x, w1, w2, {}, "none", "none", None)
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
 
 
-@pytest.mark.parametrize("shape", [(2, 20, 32), (2, 23, 224), (3, 37, 68)])
+@pytest.mark.parametrize("shape", [(2, 20, 32, 16), (2, 23, 224, 16), (3, 37, 68, 16), (2, 20, 32, 32),
+                                   (2, 23, 112, 32)])
 @pytest.mark.parametrize("acts,with_res", [(("relu", "relu"), True), (("relu", "relu"), False),
                                            (("relu6", "silu"), True), (("none", "relu"), True)])
 def test_pair_block_epilogue_vs_torch(shape, acts, with_res):
     """act2(bn2(conv2(act1(bn1(conv1 x)))) + x): the BasicBlock with its identity shortcut."""
-    N, H, W = shape
-    x, w1, w2, e = make(N, H, W, 11 + H, True)
+    N, H, W, C = shape
+    x, w1, w2, e = make(N, H, W, 11 + H, True, C)
     g = torch.Generator().manual_seed(5)
-    b1 = (torch.randn(16, generator=g) * 0.1).to(DEV)
+    b1 = (torch.randn(C, generator=g) * 0.1).to(DEV)
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", bias1=b1, act1=acts[0], act2=acts[1],
                           residual=x if with_res else None, **e)
     ref = torch_chain(x, w1, w2, e, acts[0], acts[1], x if with_res else None, "po2+", bias1=b1)
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
 
 
-def test_pair_equals_two_fused_calls():
+@pytest.mark.parametrize("C,W", [(16, 224), (32, 112)])
+def test_pair_equals_two_fused_calls(C, W):
     """The same result as qconv2d_fused twice (its row kernel: same bf16x3 arithmetic)."""
-    x, w1, w2, e = make(4, 40, 224, 3, True)
+    x, w1, w2, e = make(4, 40, W, 3, True, C)
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2", act1="relu", act2="relu", residual=x, **e)
     h = _lib.qconv2d_fused(x, w1, None, 1, 1, 1, 1, 4, "po2", post_scale=e["post_scale1"],
                            post_shift=e["post_shift1"], act="relu")
@@ -87,23 +91,25 @@ def test_pair_equals_two_fused_calls():
     assert nerr(y, y2) <= 1e-6, nerr(y, y2)
 
 
-def test_pair_full_size():
-    """BASELINE size (bs = 256 @224): every image against torch's fp32 chain."""
+@pytest.mark.parametrize("C,H", [(16, 224), (32, 112)])
+def test_pair_full_size(C, H):
+    """BASELINE size (bs = 256 @224: stage 1, and stage 2 @112): against torch's fp32 chain."""
     torch.manual_seed(0)
-    x = torch.relu(torch.randn(256, 16, 224, 224, device=DEV))
-    w1 = torch.randn(16, 16, 3, 3, device=DEV) * 0.12
-    w2 = torch.randn(16, 16, 3, 3, device=DEV) * 0.12
+    x = torch.relu(torch.randn(256, C, H, H, device=DEV))
+    w1 = torch.randn(C, C, 3, 3, device=DEV) * (0.12 if C == 16 else 0.08)
+    w2 = torch.randn(C, C, 3, 3, device=DEV) * (0.12 if C == 16 else 0.08)
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
     ref = torch_chain(x, w1, w2, {}, "none", "none", None)
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
 
 
 def test_pair_rejects():
-    x = torch.randn(1, 32, 8, 8, device=DEV)
-    w = torch.randn(32, 32, 3, 3, device=DEV)
+    x = torch.randn(1, 64, 8, 8, device=DEV)
+    w = torch.randn(64, 64, 3, 3, device=DEV)
     assert not _lib.pair_supported(x.shape)
     assert _lib.pair_supported((256, 16, 224, 224)) and not _lib.pair_supported((256, 16, 32, 32))
-    with pytest.raises(_lib.Po2qError, match="16 channels"):
+    assert _lib.pair_supported((256, 32, 112, 112)) and not _lib.pair_supported((256, 32, 16, 16))
+    with pytest.raises(_lib.Po2qError, match="16 or 32 channels"):
         _lib.qconv2d_pair(x, w, w)
     x = torch.randn(1, 16, 8, 10, device=DEV)
     w = torch.randn(16, 16, 3, 3, device=DEV)
