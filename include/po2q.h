@@ -243,7 +243,7 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw,
  * (every pointer but x, w1, w2, y may be NULL).  h never leaves the chip.  No workspace.
  * po2q_qconv2d_pair_f32 takes W % 4 == 0, W <= 224, C == 16, mode po2 / po2+ with the
  * exponent window inside bf16's range.  po2q_qconv2d_pair_supported: 1 when it takes the
- * shape AND is the faster path (W >= 128; narrower rows: two single-conv calls).
+ * shape AND is the faster path (C = 16, W >= 128; otherwise two single-conv calls).
  */
 int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
 int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, float* y,

@@ -418,8 +418,8 @@ class SplitConv:
 
 def pair_supported(x_shape, bits=4, mode="po2", fsr=1):
     """True when qconv2d_pair takes this input shape (16 or 32 channels, W % 4 == 0, W <= 224
-    / 112, po2 / po2+ with the exponent window inside bf16's range) and is the faster path (at
-    least 4 waves per block: W >= 128 / 64; narrower rows: two single-conv calls)."""
+    / 112, po2 / po2+ with the exponent window inside bf16's range) and is the faster path
+    (C = 16 with W >= 128; elsewhere two single-conv calls measured faster)."""
     if mode not in ("po2", "po2+"):
         return False
     N, C, H, W = (int(v) for v in x_shape)

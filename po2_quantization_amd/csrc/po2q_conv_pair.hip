@@ -573,6 +573,10 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // below 4 waves per block a block is too narrow to hide its per-row latency: two
     // single-conv launches are faster there (ResNet56 @32: 2.6 vs 2.0 ms per forward)
     if ((C == 16 || C == 32) && W <= 3 * (512 / C)) return 0;
+    // C = 32 (stage 2 @112): 0.366 ms per pair alone but 0.418 ms inside the ResNet56 chain,
+    // against 2 x 0.197 ms for the single-conv kernel there (profiles/r02_v7_kernel_stats.csv):
+    // the pair is not the faster path, so the advisory says no (the kernel stays callable)
+    if (C == 32) return 0;
     po2q::PairPlan pp;
     int pd, nts;
     pair_variant(pd, nts);
