@@ -384,10 +384,16 @@ hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
                                  int act, hipStream_t s, const WQuant& q);
 
+// stride-2 full-row blocks (po2q_conv_rows2.hip: 3x3 s2 16 -> 32, plan vrx = 5)
+void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
+                             const float* ps, const float* pb, int act, bool epi, const WQuant& q);
+
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;
     rowsk_candidates(base, mode, bits, fsr, out);
     rowsf_candidates(base, mode, bits, fsr, out);
+    rows2_candidates(base, mode, bits, fsr, out);
     if (mode == 0 || b.groups != 1) return;
     if (bits < 1 || bits > 16) return;
     const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
@@ -497,6 +503,7 @@ static hipError_t rows_dispatch(const ConvPlan& p, const float* x, const uint16_
 
 hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                    const float* bias, float* y, hipStream_t s, const WQuant& q) {
+    if (p.vrx == 5) return launch_conv_rows2(p, x, bias, y, s, nullptr, nullptr, 0, false, q);
     if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false, q);
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, nullptr, nullptr, 0, false, q);
     if (p.fp) return hipErrorInvalidValue;  // fused weight staging: full-row / C = 64 plans only
@@ -536,6 +543,7 @@ namespace po2q {
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s, const WQuant& q) {
+    if (p.vrx == 5) return launch_conv_rows2(p, x, bias, y, s, ps, pb, act, true, q);
     if (p.vrx == 4) return launch_conv_rowsf(p, x, packed, scale, bias, y, s, ps, pb, act, true, q);
     if (p.vrx) return launch_conv_rowsk(p, x, packed, scale, bias, y, s, ps, pb, act, true, q);
     if (p.fp) return hipErrorInvalidValue;

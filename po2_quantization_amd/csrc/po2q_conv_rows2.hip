@@ -1,0 +1,369 @@
+// bf16x3 full-row-block conv for the stride-2 3x3 / pad-1 transition layers with C = 16 ->
+// K = 32 (ResNet56 layer2.0.conv1 at 224x224 -> 112x112; reference resnet.py:55-71, the
+// first BasicBlock of a stage, each conv QuantizedConv2d.forward, quantized_conv.py:32-38).
+//
+// Same arithmetic as the other bf16x3 kernels (exact +-2^e bf16 weights x exact 3-way bf16
+// split of the fp32 activations, fp32 accumulation on v_mfma_f32_16x16x32_bf16) and the
+// same walk as conv_rowsf (po2q_conv_rowsf.hip): a block owns (image, segment of RB output
+// rows) across the whole width, each input row is one cooperative whole-row LDS-DMA into a
+// PD-slot ring, one s_barrier per input row, hand-counted vmcnt.  What stride 2 changes:
+//   * wave w owns 16 output columns 16w .. 16w + 15, i.e. input columns 32w - 1 .. 32w + 31;
+//     it splits them into an EVEN and an ODD sub-plane ([17 | 16 pixels][C] bf16), so the
+//     tap-s pixel of output column p (input column 2p + s - 1) is E[p], O[p], E[p + 1] for
+//     s = 0, 1, 2 -- 16 consecutive pixels of one sub-plane, conflict-free like stride 1;
+//   * each input row feeds at most two output rows: an even-offset row adds tap row 1 to
+//     output t, an odd-offset row adds tap row 2 to output t - 1 (which completes it) and
+//     tap row 0 to output t: two accumulator slots rotate, output rows are stored every
+//     other step (the steps between issue dropped stores, so the vmcnt count holds);
+//   * both weights are quantized + packed by the block into LDS (fused staging): one launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <type_traits>
+#include <vector>
+
+#include "po2q_epi.h"
+#include "po2q_internal.h"
+#include "po2q_quant_dev.h"
+#include "po2q_rows_dev.h"
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+namespace {
+constexpr int kR2EP = 17, kR2OP = 16;                          // even / odd sub-plane pixels
+template <int CC> constexpr int kR2Plane = (kR2EP + kR2OP) * 2 * CC + 32;  // + zero slot
+template <int CC> constexpr int kR2KS = CC == 16 ? 2 : 3;
+}  // namespace
+
+struct Rows2Args {
+    int N, H, W, P, Q;
+    int RB, nseg, items, remap;
+    int rawslot;       // bytes per raw ring slot (>= ND x waves KiB: the DMAs past the row land in it)
+    const float* ps;   // fused epilogue (EPI): y = act(y * ps[k] + pb[k]); either may be NULL
+    const float* pb;
+    int act;
+    WQuant q;
+};
+
+template <int CC, int PD, bool EPI, int NTS, int ND>
+__global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x, const float* __restrict__ bias,
+                                                     float* __restrict__ y, Rows2Args a) {
+    static_assert(CC == 16 || CC == 32, "C = 16 or 32");
+    static_assert(PD == 2 || PD == 4, "ring slots: 4 % PD == 0 keeps every index static");
+    constexpr int K = 2 * CC, NT = K / 16, KS = kR2KS<CC>, NF = 3 * KS * NT;
+    constexpr int PL = kR2Plane<CC>, OBASE = kR2EP * 2 * CC, ZOFF = (kR2EP + kR2OP) * 2 * CC;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nw = (int)(blockDim.x >> 6);
+    uint4* wl = reinterpret_cast<uint4*>(lds);                    // [NF][64] B fragments
+    unsigned char* raw = lds + NF * 1024;                         // PD slots [C][W] fp32
+    unsigned char* slab = raw + PD * a.rawslot + wave * (3 * PL);  // this wave's planes
+
+    int blk = blockIdx.x;
+    if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
+    if (blk >= a.items) return;  // block-uniform
+    const int seg = blk % a.nseg;
+    const int n = blk / a.nseg;
+    const int p0 = seg * a.RB;
+    const int rbe = min(a.RB, a.P - p0);
+    const int nrows = 2 * rbe + 1;  // input rows 2 p0 - 1 .. 2 (p0 + rbe) - 1
+    const int q0 = 16 * wave;       // first output column of the wave
+
+    // ---- DMA: lane l of this wave's instruction i -> float4 e = 64 (ndma w + i) + l of the
+    // row's C x W/4 float4 (e past the row: out-of-range zeros into the slot's padding)
+    const int HW = a.H * a.W;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
+    const int W4 = a.W >> 2;
+    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    auto load_row = [&](int sl, int jn) __attribute__((always_inline)) {
+        const int h = 2 * p0 - 1 + jn;
+        const bool hok = jn < nrows && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t base = raw_lds + (uint32_t)(sl * a.rawslot) + (uint32_t)(ND * wave) * 1024u;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const int e = 64 * (ND * wave + i) + lane;
+            const int c = e / W4, q = 4 * (e - c * W4);
+            const uint32_t vo = (hok && c < CC) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u + roff : 0x7fffffffu;
+            rows_dma16<false>(rs, vo, 0u, base + i * 1024u);
+        }
+    };
+
+    // ---- split tasks: (input column 2 q0 + t, channel octet o), t < 32; lane + 64 k
+    constexpr int NTASK = 4 * CC / 64;  // 1 or 2 per lane
+    int rd[NTASK], wa[NTASK];
+    bool tok[NTASK];
+#pragma unroll
+    for (int k = 0; k < NTASK; ++k) {
+        const int id = lane + 64 * k;
+        const int t = id & 31, o = id >> 5;
+        const int col = 2 * q0 + t;
+        tok[k] = col < a.W;
+        rd[k] = (o * 8) * (a.W * 4) + (tok[k] ? col : 0) * 4;
+        // local index t + 1: odd t -> even pixel (t + 1) / 2, even t -> odd pixel t / 2
+        wa[k] = (t & 1) ? x_addr<CC>((t + 1) >> 1, o) : OBASE + x_addr<CC>(t >> 1, o);
+    }
+    // left halo column 2 q0 - 1 -> even pixel 0 (lanes < C: one channel each)
+    const int hcol = 2 * q0 - 1;
+    const bool h_ok = lane < CC && hcol >= 0;
+    const int rd_h = (lane % CC) * (a.W * 4) + (h_ok ? hcol : 0) * 4;
+    const int wa_h = x_addr<CC>(0, (lane % CC) >> 3) + ((lane % CC) & 7) * 2;
+
+    // ---- A fragment offsets per k-step (E[p], O[p], E[p+1] for taps 0, 1, 2)
+    int aoff[KS];
+    {
+        const int p = lane & 15, g = lane >> 4;
+        if constexpr (CC == 16) {
+            aoff[0] = g < 2 ? x_addr<16>(p, g) : OBASE + x_addr<16>(p, g - 2);
+            aoff[1] = g < 2 ? x_addr<16>(p + 1, g) : ZOFF;
+        } else {
+            aoff[0] = x_addr<32>(p, g);
+            aoff[1] = OBASE + x_addr<32>(p, g);
+            aoff[2] = x_addr<32>(p + 1, g);
+        }
+    }
+
+    const int PQ = a.P * a.Q;
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * K * PQ, K * PQ * 4);
+    constexpr int ST = NT;  // stores per step (every step; odd steps' are dropped)
+
+    float scale = 1.0f;
+    bool fin = true;
+    float bk[NT], eps_[NT], epb_[NT];
+    floatx4 acc[2][NT];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[sl][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // MFMAs of the split row with tap row rr into accumulator slot SLOT
+    auto mfmas = [&](auto RR_, auto SLOT_) __attribute__((always_inline)) {
+        constexpr int RR = decltype(RR_)::value, SLOT = decltype(SLOT_)::value;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                af[pl] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slab + pl * PL + aoff[ks]));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const bf16x8 b = __builtin_bit_cast(bf16x8, wl[((RR * KS + ks) * NT + nt) * 64 + lane]);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    acc[SLOT][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl], b, acc[SLOT][nt], 0, 0, 0);
+            }
+        }
+    };
+    // store output row p0 + o from slot SLOT (dropped when `valid` is false), then zero it
+    auto store_row = [&](auto SLOT_, int o, bool valid) __attribute__((always_inline)) {
+        constexpr int SLOT = decltype(SLOT_)::value;
+        const bool orow = valid && o >= 0 && o < rbe;
+        const int g = lane >> 4;
+        const int q = q0 + 4 * g;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int k = 16 * nt + (lane & 15);
+            floatx4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float t = acc[SLOT][nt][e] * scale + bk[nt];
+                if constexpr (EPI) t = epi_act(t * eps_[nt] + epb_[nt], a.act);
+                v[e] = t;
+            }
+            const uint32_t yo = (uint32_t)k * (uint32_t)PQ + (uint32_t)(orow ? p0 + o : 0) * a.Q + (uint32_t)q;
+            rows_store<(NTS & 1) != 0>(ry, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
+            if (valid) acc[SLOT][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    // vm ops after this wave's DMAs of row j (issued in step j - PD + 1, after its barrier)
+    // until the wait of step j: that step's ST stores, then ND DMAs + ST stores per step
+    constexpr int VMW = ST + (PD - 2) * (ND + ST);
+    auto step = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S4 = decltype(S_)::value;  // j % 4
+        constexpr int RS = S4 % PD;
+        rows_wait<VMW>();
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs of row j landed; row j - 1 is split
+        load_row((S4 + PD - 1) % PD, j - 1 + PD);
+        // split input row j: the wave's 32 columns (+ the left halo column)
+        {
+            const unsigned char* rw = raw + RS * a.rawslot;
+#pragma unroll
+            for (int k = 0; k < NTASK; ++k) {
+                uint32_t b8[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) b8[e] = *reinterpret_cast<const uint32_t*>(rw + rd[k] + e * (a.W * 4));
+                if (!tok[k]) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) b8[e] = 0u;
+                }
+                uint4 hi, mid, lo;
+                split3(b8, hi, mid, lo);
+                *reinterpret_cast<uint4*>(slab + wa[k]) = hi;
+                *reinterpret_cast<uint4*>(slab + PL + wa[k]) = mid;
+                *reinterpret_cast<uint4*>(slab + 2 * PL + wa[k]) = lo;
+            }
+            if (lane < CC) {
+                uint32_t hb = *reinterpret_cast<const uint32_t*>(rw + rd_h);
+                hb = h_ok ? hb : 0u;
+                uint16_t h16, m16, l16;
+                split1(hb, h16, m16, l16);
+                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+                *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
+                *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
+            }
+        }
+        // input row j: even j = 2t -> tap row 0 into output t, tap row 2 into output t - 1
+        // (complete: stored); odd j = 2t + 1 -> tap row 1 into output t
+        const int t = j >> 1;
+        if constexpr ((S4 & 1) == 0) {
+            constexpr int CUR = (S4 >> 1) & 1, PREV = CUR ^ 1;
+            mfmas(std::integral_constant<int, 2>{}, std::integral_constant<int, PREV>{});
+            mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, CUR>{});
+            store_row(std::integral_constant<int, PREV>{}, t - 1, true);
+        } else {
+            constexpr int CUR = (S4 >> 1) & 1;
+            mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, CUR>{});
+            store_row(std::integral_constant<int, CUR>{}, t, false);  // dropped: keeps the count
+        }
+    };
+
+    {
+        const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < PD - 1; ++r) {
+            load_row(r, r);
+#pragma unroll
+            for (int i = 0; i < ST; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
+        }
+    }
+    // ---- weights: quantize + pack into LDS while those DMAs fly (scratch: wave 0's planes)
+    {
+        unsigned* red = reinterpret_cast<unsigned*>(raw + PD * a.rawslot);
+        unsigned* thr = red + 16;
+        scale = wq_prologue(a.q, thr, red, nw, fin);
+        __syncthreads();  // every wave's scratch reads done before wl (disjoint) -- and thr stays
+        for (int e = tid; e < NF * 64; e += blockDim.x) wl[e] = wq_frag_rows(a.q, CC, K, CC, NT, KS, e, scale, fin, thr);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int k = 16 * nt + (lane & 15);
+            bk[nt] = bias ? bias[k] : 0.0f;
+            eps_[nt] = (EPI && a.ps) ? a.ps[k] : 1.0f;
+            epb_[nt] = (EPI && a.pb) ? a.pb[k] : 0.0f;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(bk[nt]), "+v"(eps_[nt]), "+v"(epb_[nt]));
+        __syncthreads();  // wl complete, scratch free
+        if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + ZOFF) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    // the last output row completes (and is stored) at step nrows - 1 = 2 rbe
+    for (int j = 0; j < nrows; j += 4) {
+        step(std::integral_constant<int, 0>{}, j);
+        step(std::integral_constant<int, 1>{}, j + 1);
+        if (j + 2 >= nrows) break;
+        step(std::integral_constant<int, 2>{}, j + 2);
+        step(std::integral_constant<int, 3>{}, j + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
+}
+
+// ------------------------------------------------------------------ planning --
+static size_t rows2_lds(int C, int waves, int pd, int rawslot) {
+    const int nf = 3 * (C == 16 ? 2 : 3) * (2 * C / 16);
+    const int plane = (kR2EP + kR2OP) * 2 * C + 32;
+    return (size_t)nf * 1024 + (size_t)pd * rawslot + (size_t)waves * 3 * plane;
+}
+
+void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
+    if (mode == 0 || b.groups != 1) return;
+    if (bits < 1 || bits > 16) return;
+    const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
+    if (lo < -126 || hi > 127) return;  // +-2^e must be a normal bf16
+    if (b.R != 3 || b.S != 3 || b.sh != 2 || b.sw != 2 || b.ph != 1 || b.pw != 1 || b.dh != 1 || b.dw != 1) return;
+    if (b.C != 16 || b.K != 32) return;  // the instantiated shape (ResNet layer2.0.conv1)
+    if (b.W % 4 != 0 || b.Q % 4 != 0) return;
+    const int waves = (b.Q + 15) / 16;
+    if (waves < 1 || waves > 7 || 32 * waves < b.W) return;  // the waves' input strips cover the row
+    if ((int64_t)b.C * b.H * b.W * 4 >= (1LL << 31) || (int64_t)b.K * b.P * b.Q * 4 >= (1LL << 31)) return;
+    if ((int64_t)b.K * b.C * 9 > 65536) return;  // fused staging: every block reads the weight
+    ConvPlan p = b;
+    p.kind = KIND_BF16X3_ROWS;
+    p.vrx = 5;  // stride-2 full-row blocks
+    p.CC = b.C; p.NT = b.K / 16; p.NJ = 1; p.TQ = 16 * waves;
+    p.steps = b.C == 16 ? 2 : 3; p.nchunks = 1; p.kblocks = 1; p.taps = 9;
+    p.PS = 0; p.MI = 0; p.fp = 1;
+    p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = p.dma_ov = 0;
+    p.HH = 0; p.WW = p.WWp = 33;
+    p.SB = 2 * b.C;
+    p.plane = (kR2EP + kR2OP) * 2 * b.C + 32;
+    p.packed_floats = (int64_t)3 * p.steps * p.NT * 64 * 4;
+    p.tilesQ = 1;
+    const int total4 = b.C * b.W / 4;                      // float4 per input row
+    const int ndma = (total4 + 64 * waves - 1) / (64 * waves);
+    if (ndma < 1 || ndma > 2) return;  // instantiated DMA counts per wave
+    const int rawslot = std::max(b.C * b.W * 4, ndma * waves * 1024);
+    p.dma_ni = ndma;
+    p.dma_nck = rawslot;
+    for (int pd : {2, 4}) {
+        ConvPlan q = p;
+        q.pd = pd;
+        q.lds_bytes = rows2_lds(b.C, waves, pd, rawslot);
+        const int per_cu = std::min(2, (int)(160 * 1024 / q.lds_bytes));
+        if (per_cu < 1) continue;
+        // segments: every CU busy with per_cu blocks, one extra input row per segment
+        int nseg = std::max(1, (256 * per_cu + b.N - 1) / b.N);
+        nseg = std::min(nseg, std::max(1, b.P / 4));
+        for (int f : {1, 2}) {
+            ConvPlan c = q;
+            const int ns = std::min(nseg * f, std::max(1, b.P / 4));
+            c.TP = (b.P + ns - 1) / ns;
+            c.tilesP = (b.P + c.TP - 1) / c.TP;
+            c.blocks = ((int64_t)b.N * c.tilesP + 7) / 8 * 8;
+            for (int nts : {0, 1}) {
+                c.nts = nts;
+                out.push_back({0.885 + 0.001 * (f - 1) + 0.002 * nts + 0.001 * (pd - 2), c});
+            }
+            if (ns == nseg) break;
+        }
+    }
+}
+
+template <int CC, int PD, bool EPI, int NTS>
+static hipError_t launch_rows2_t(const ConvPlan& p, const Rows2Args& a, const float* x, const float* bias, float* y,
+                                 hipStream_t s) {
+    const int waves = p.TQ / 16;
+    if (p.dma_ni == 2)
+        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, 2>), dim3((unsigned)p.blocks), dim3(64 * waves), p.lds_bytes,
+                           s, x, bias, y, a);
+    else if (p.dma_ni == 1)
+        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, 1>), dim3((unsigned)p.blocks), dim3(64 * waves), p.lds_bytes,
+                           s, x, bias, y, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
+                             const float* ps, const float* pb, int act, bool epi, const WQuant& q) {
+    if (p.kind != KIND_BF16X3_ROWS || p.vrx != 5 || !q.w || p.C != 16 || p.K != 32) return hipErrorInvalidValue;
+    Rows2Args a;
+    a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
+    a.RB = p.TP; a.nseg = p.tilesP; a.items = p.N * p.tilesP;
+    a.remap = (p.blocks % 8 == 0) ? 1 : 0;
+    a.rawslot = p.dma_nck;
+    a.ps = ps; a.pb = pb; a.act = act;
+    a.q = q;
+#define PO2Q_R2(d, e, nt) \
+    if (p.pd == d && epi == e && p.nts == nt) return launch_rows2_t<16, d, e, nt>(p, a, x, bias, y, s);
+    PO2Q_R2(2, false, 0) PO2Q_R2(2, false, 1) PO2Q_R2(4, false, 0) PO2Q_R2(4, false, 1)
+    PO2Q_R2(2, true, 0) PO2Q_R2(2, true, 1) PO2Q_R2(4, true, 0) PO2Q_R2(4, true, 1)
+#undef PO2Q_R2
+    return hipErrorInvalidValue;
+}
+
+}  // namespace po2q

@@ -93,6 +93,12 @@ SHAPES = [
     # C = K = 64 (output channels across a block's waves): ragged strip, short segment
     (2, 64, 12, 40, 64, 3, 3, 1, 1, 1, 1),
     (1, 64, 3, 8, 64, 3, 3, 1, 1, 1, 1),
+    # stride-2 full-row kernel (16 -> 32): two waves with a ragged strip, odd rows, one wave
+    # with one DMA per row, a wide image
+    (2, 16, 40, 40, 32, 3, 3, 2, 1, 1, 1),
+    (1, 16, 9, 64, 32, 3, 3, 2, 1, 1, 1),
+    (1, 16, 17, 8, 32, 3, 3, 2, 1, 1, 1),
+    (2, 16, 30, 224, 32, 3, 3, 2, 1, 1, 1),
 ]
 
 
@@ -253,6 +259,7 @@ FUSED_SHAPES = [  # (N, C, H, W, K, R, stride, pad, groups): row kernels, K-spli
     (2, 16, 33, 31, 32, 3, 2, 1, 1),
     (2, 32, 16, 16, 64, 1, 2, 0, 1),
     (2, 96, 9, 9, 96, 3, 1, 1, 96),
+    (2, 16, 40, 40, 32, 3, 2, 1, 1),
 ]
 
 
