@@ -1,6 +1,7 @@
-// bf16x3 full-row-block conv for the stride-2 3x3 / pad-1 transition layers with C = 16 ->
-// K = 32 (ResNet56 layer2.0.conv1 at 224x224 -> 112x112; reference resnet.py:55-71, the
-// first BasicBlock of a stage, each conv QuantizedConv2d.forward, quantized_conv.py:32-38).
+// bf16x3 full-row-block conv for the stride-2 3x3 / pad-1 transition layers, C -> K = 2C with
+// C = 16 or 32 (ResNet56 layer2.0.conv1 at 224x224 -> 112x112 and layer3.0.conv1 at 112x112
+// -> 56x56; reference resnet.py:55-71, the first BasicBlock of a stage, each conv
+// QuantizedConv2d.forward, quantized_conv.py:32-38).
 //
 // Same arithmetic as the other bf16x3 kernels (exact +-2^e bf16 weights x exact 3-way bf16
 // split of the fp32 activations, fp32 accumulation on v_mfma_f32_16x16x32_bf16) and the
@@ -285,7 +286,8 @@ void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
     const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
     if (lo < -126 || hi > 127) return;  // +-2^e must be a normal bf16
     if (b.R != 3 || b.S != 3 || b.sh != 2 || b.sw != 2 || b.ph != 1 || b.pw != 1 || b.dh != 1 || b.dw != 1) return;
-    if (b.C != 16 || b.K != 32) return;  // the instantiated shape (ResNet layer2.0.conv1)
+    // the instantiated shapes: ResNet56 layer2.0.conv1 (16 -> 32) and layer3.0.conv1 (32 -> 64)
+    if (!((b.C == 16 && b.K == 32) || (b.C == 32 && b.K == 64))) return;
     if (b.W % 4 != 0 || b.Q % 4 != 0) return;
     const int waves = (b.Q + 15) / 16;
     if (waves < 1 || waves > 7 || 32 * waves < b.W) return;  // the waves' input strips cover the row
@@ -305,11 +307,12 @@ void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
     p.tilesQ = 1;
     const int total4 = b.C * b.W / 4;                      // float4 per input row
     const int ndma = (total4 + 64 * waves - 1) / (64 * waves);
-    if (ndma < 1 || ndma > 2) return;  // instantiated DMA counts per wave
+    if (ndma < 1 || ndma > (b.C == 16 ? 2 : 4)) return;  // instantiated DMA counts per wave
     const int rawslot = std::max(b.C * b.W * 4, ndma * waves * 1024);
     p.dma_ni = ndma;
     p.dma_nck = rawslot;
     for (int pd : {2, 4}) {
+        if (b.C == 32 && pd != 2) continue;  // C = 32: one block per CU already at pd 2 (LDS)
         ConvPlan q = p;
         q.pd = pd;
         q.lds_bytes = rows2_lds(b.C, waves, pd, rawslot);
@@ -318,39 +321,49 @@ void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
         // segments: every CU busy with per_cu blocks, one extra input row per segment
         int nseg = std::max(1, (256 * per_cu + b.N - 1) / b.N);
         nseg = std::min(nseg, std::max(1, b.P / 4));
+        int prev = -1;
         for (int f : {1, 2}) {
             ConvPlan c = q;
             const int ns = std::min(nseg * f, std::max(1, b.P / 4));
+            if (ns == prev) break;
+            prev = ns;
             c.TP = (b.P + ns - 1) / ns;
             c.tilesP = (b.P + c.TP - 1) / c.TP;
             c.blocks = ((int64_t)b.N * c.tilesP + 7) / 8 * 8;
             for (int nts : {0, 1}) {
+                if (b.C == 32 && nts) continue;
                 c.nts = nts;
                 out.push_back({0.885 + 0.001 * (f - 1) + 0.002 * nts + 0.001 * (pd - 2), c});
             }
-            if (ns == nseg) break;
         }
     }
+}
+
+template <int CC, int PD, bool EPI, int NTS, int ND>
+static hipError_t launch_rows2_nd(const ConvPlan& p, const Rows2Args& a, const float* x, const float* bias, float* y,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND>), dim3((unsigned)p.blocks), dim3(64 * (p.TQ / 16)),
+                       p.lds_bytes, s, x, bias, y, a);
+    return hipGetLastError();
 }
 
 template <int CC, int PD, bool EPI, int NTS>
 static hipError_t launch_rows2_t(const ConvPlan& p, const Rows2Args& a, const float* x, const float* bias, float* y,
                                  hipStream_t s) {
-    const int waves = p.TQ / 16;
-    if (p.dma_ni == 2)
-        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, 2>), dim3((unsigned)p.blocks), dim3(64 * waves), p.lds_bytes,
-                           s, x, bias, y, a);
-    else if (p.dma_ni == 1)
-        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, 1>), dim3((unsigned)p.blocks), dim3(64 * waves), p.lds_bytes,
-                           s, x, bias, y, a);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+    switch (p.dma_ni) {
+        case 1: return launch_rows2_nd<CC, PD, EPI, NTS, 1>(p, a, x, bias, y, s);
+        case 2: return launch_rows2_nd<CC, PD, EPI, NTS, 2>(p, a, x, bias, y, s);
+        case 3: if constexpr (CC == 32) return launch_rows2_nd<CC, PD, EPI, NTS, 3>(p, a, x, bias, y, s); break;
+        case 4: if constexpr (CC == 32) return launch_rows2_nd<CC, PD, EPI, NTS, 4>(p, a, x, bias, y, s); break;
+        default: break;
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
                              const float* ps, const float* pb, int act, bool epi, const WQuant& q) {
-    if (p.kind != KIND_BF16X3_ROWS || p.vrx != 5 || !q.w || p.C != 16 || p.K != 32) return hipErrorInvalidValue;
+    if (p.kind != KIND_BF16X3_ROWS || p.vrx != 5 || !q.w || !((p.C == 16 && p.K == 32) || (p.C == 32 && p.K == 64)))
+        return hipErrorInvalidValue;
     Rows2Args a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.items = p.N * p.tilesP;
@@ -359,10 +372,12 @@ hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bia
     a.ps = ps; a.pb = pb; a.act = act;
     a.q = q;
 #define PO2Q_R2(d, e, nt) \
-    if (p.pd == d && epi == e && p.nts == nt) return launch_rows2_t<16, d, e, nt>(p, a, x, bias, y, s);
+    if (p.C == 16 && p.pd == d && epi == e && p.nts == nt) return launch_rows2_t<16, d, e, nt>(p, a, x, bias, y, s);
     PO2Q_R2(2, false, 0) PO2Q_R2(2, false, 1) PO2Q_R2(4, false, 0) PO2Q_R2(4, false, 1)
     PO2Q_R2(2, true, 0) PO2Q_R2(2, true, 1) PO2Q_R2(4, true, 0) PO2Q_R2(4, true, 1)
 #undef PO2Q_R2
+    if (p.C == 32 && p.pd == 2 && p.nts == 0)
+        return epi ? launch_rows2_t<32, 2, true, 0>(p, a, x, bias, y, s) : launch_rows2_t<32, 2, false, 0>(p, a, x, bias, y, s);
     return hipErrorInvalidValue;
 }
 

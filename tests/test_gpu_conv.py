@@ -99,6 +99,9 @@ SHAPES = [
     (1, 16, 9, 64, 32, 3, 3, 2, 1, 1, 1),
     (1, 16, 17, 8, 32, 3, 3, 2, 1, 1, 1),
     (2, 16, 30, 224, 32, 3, 3, 2, 1, 1, 1),
+    (2, 32, 40, 40, 64, 3, 3, 2, 1, 1, 1),   # the same kernel, 32 -> 64
+    (1, 32, 17, 8, 64, 3, 3, 2, 1, 1, 1),
+    (2, 32, 30, 112, 64, 3, 3, 2, 1, 1, 1),
 ]
 
 

@@ -72,6 +72,7 @@ for s in $STEPS; do
         sweep) run sweep 900 python tools/tile_sweep.py ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep1) run sweep1 600 python tools/tile_sweep.py --shapes 1 --iters 21 ;;
+        sweep4) run sweep4 600 python tools/tile_sweep.py --shapes 4 --iters 21 ;;
         sweep0) run sweep0 600 python tools/tile_sweep.py --shapes 0 --iters 21 ;;
         sweep3) run sweep3 600 python tools/tile_sweep.py --shapes 3 --iters 21 ;;
         sweep6) run sweep6 600 python tools/tile_sweep.py --shapes 6 --iters 21 ;;
