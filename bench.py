@@ -75,6 +75,7 @@ class QConvChain:
         self.timed_layer = None      # index of the layer whose launches are timed
         self.events = []
         self.pair = True             # conv1 -> conv2 of stage-1 / stage-2 blocks as one pair launch
+        self.s2ds = True             # stride-2 conv1 + its 1x1 shortcut of a stage's first block as one launch
 
     def conv(self, i, x):
         _, C, K, R, st, pad, _ = self.layers[i]
@@ -96,17 +97,28 @@ class QConvChain:
             has_ds = i + 2 < len(self.layers) and self.layers[i + 2][6] == "ds"
             if self.pairable(i, x):
                 out = self._timed_pair(i, x, record)
+            elif has_ds and self.s2ds_ok(i, x):
+                # stride-2 conv1 and the projection shortcut (its output feeds the add) on one read of x
+                out, _ = _lib.qconv2d_s2ds(x, self.weights[i], self.weights[i + 2], self.bits, self.mode)
+                out = self._timed(i + 1, out, record)
             else:
                 out = self._timed(i, x, record)
                 out = self._timed(i + 1, out, record)
             if has_ds:
-                self._timed(i + 2, x, record)  # projection shortcut (its output feeds the add)
+                if not self.s2ds_ok(i, x):
+                    self._timed(i + 2, x, record)  # projection shortcut (its output feeds the add)
                 i += 3
             else:
                 i += 2
             x = out
         pooled = x.mean(dim=(2, 3))
         return torch.nn.functional.linear(pooled, self.fc_w, self.fc_b)
+
+    def s2ds_ok(self, i, x):
+        """conv1 (3x3 s2 C -> 2C) and downsample.0 (1x1 s2 C -> 2C) of block i as ONE launch."""
+        (_, C, K, R, st, _, _), (_, C3, K3, R3, st3, _, _) = self.layers[i], self.layers[i + 2]
+        return self.s2ds and (K, R, st, C3, K3, R3, st3) == (2 * C, 3, 2, C, 2 * C, 1, 2) \
+            and self.mode in ("po2", "po2+") and _lib.s2ds_supported(x.shape, self.bits, self.mode)
 
     def pair_call(self, i, x):
         return _lib.qconv2d_pair(x, self.weights[i], self.weights[i + 1], self.bits, self.mode)
@@ -246,6 +258,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pair", action="store_true",
                     help="run every conv as its own launch (no stage-1 conv1->conv2 pair kernel)")
+    ap.add_argument("--no-s2ds", action="store_true",
+                    help="run a stage's stride-2 conv1 and its 1x1 shortcut as two launches (each reads x)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="use the heuristic plans instead of autotuning each conv shape on first use")
     args = ap.parse_args()
@@ -271,6 +285,7 @@ def main():
     chain = QConvChain(n_blocks, args.classes, args.quantizer, args.bits, args.precision, dev, seed=0)
     chain.timed_layer = 1  # layer1.0.conv2: 3x3 16->16 at full resolution (dominant shape)
     chain.pair = not args.no_pair
+    chain.s2ds = not args.no_s2ds
     B, Hs = args.batch, args.image
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
     gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
@@ -302,6 +317,8 @@ def main():
     # dominant op (HIP events on its stream): the stage-1 conv pair (conv1 -> conv2 of a block
     # in one launch) when the chain runs pairs, else the fused quantize+conv of the timed shape
     pair_used = chain.pairable(0, x)
+    s2ds_used = chain.s2ds and args.quantizer in ("po2", "po2+") and \
+        _lib.s2ds_supported((B, 16, Hs, Hs), args.bits, args.quantizer)
     xl = torch.relu(torch.randn(args.batch, 16, args.image, args.image, device=dev))
 
     def launch_avg_ms(fn, reps=20):
@@ -394,11 +411,14 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
-        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s"
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
-                                  " (stage-1/2 conv1->conv2 pairs as one launch each)" if pair_used else "",
+                                  " (stage-1 conv1->conv2 pairs as one launch each)" if pair_used else "",
+                                  " (stride-2 conv1 + 1x1 shortcut of stages 2-3 as one launch each)"
+                                  if s2ds_used else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "conv_pairs": pair_used,
+                   "s2ds": s2ds_used,
                    "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
                    "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world, "world_size": world,

@@ -253,6 +253,24 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
                           const float* post_scale2, const float* post_shift2, const float* residual, int act2,
                           void* stream);
 
+/*
+ * The stride-2 transition of a ResNet56 stage (reference models/resnet.py:55-71 with the
+ * projection shortcut: conv1 = QuantizedConv2d(C, 2C, 3, stride 2, padding 1) and
+ * downsample.0 = QuantizedConv2d(C, 2C, 1, stride 2, padding 0), both
+ * QuantizedConv2d.forward, models/quantized_conv.py:32-38, on the same x) in one launch:
+ *   y   = act((conv3x3_s2(x, Q(w)))   * post_scale    + post_shift)
+ *   yds =     conv1x1_s2(x, Q(wds))   * post_scale_ds + post_shift_ds
+ * x [N, C, H, W], w [2C, C, 3, 3], wds [2C, C, 1, 1] (each quantized with its own max|w|,
+ * the same bits / fsr / mode), y and yds [N, 2C, P, Q]; x is read once for both.  Every
+ * epilogue pointer may be NULL.  C = 16 or 32, W % 4 == 0, po2 / po2+; no workspace.
+ * po2q_qconv2d_s2ds_supported: 1 when the shape takes it.
+ */
+int po2q_qconv2d_s2ds_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
+int po2q_qconv2d_s2ds_f32(const float* x, const float* w, const float* wds, float* y, float* yds,
+                          int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode,
+                          const float* post_scale, const float* post_shift, int act,
+                          const float* post_scale_ds, const float* post_shift_ds, void* stream);
+
 typedef struct po2q_conv_plan po2q_conv_plan;
 int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index,
                              int64_t N, int64_t C, int64_t H, int64_t W,

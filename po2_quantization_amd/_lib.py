@@ -53,6 +53,8 @@ EXPORTS = (
     "po2q_qconv2d_wgrad_f32",
     "po2q_qconv2d_pair_supported",
     "po2q_qconv2d_pair_f32",
+    "po2q_qconv2d_s2ds_supported",
+    "po2q_qconv2d_s2ds_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -141,6 +143,8 @@ def load():
     L.po2q_qconv2d_describe.argtypes = [i64] * 14 + [i32, i32, i32, i32, ctypes.c_char_p, sz]
     L.po2q_qconv2d_pair_supported.restype = i32
     L.po2q_qconv2d_pair_supported.argtypes = [i64] * 4 + [i32] * 3
+    L.po2q_qconv2d_s2ds_supported.restype = i32
+    L.po2q_qconv2d_s2ds_supported.argtypes = [i64] * 4 + [i32] * 3
     _lib = L
     return L
 
@@ -440,6 +444,31 @@ def qconv2d_pair(x, w1, w2, bits=4, mode="po2", fsr=1, bias1=None, bias2=None, p
         raise Po2qError("po2q: qconv2d_pair needs the operator library (PO2Q_LIB selects another build)")
     return _op_call(O.qconv2d_pair, x, w1, w2, int(bits), MODES[mode], int(fsr), bias1, bias2, post_scale1,
                     post_shift1, ACTS[act1], post_scale2, post_shift2, residual, ACTS[act2])
+
+
+def s2ds_supported(x_shape, bits=4, mode="po2", fsr=1):
+    """True when qconv2d_s2ds takes this input shape (C = 16 or 32 -> 2C, W % 4 == 0, po2 / po2+)."""
+    if mode not in ("po2", "po2+"):
+        return False
+    N, C, H, W = (int(v) for v in x_shape)
+    return bool(load().po2q_qconv2d_s2ds_supported(N, C, H, W, int(bits), int(fsr), MODES[mode]))
+
+
+def qconv2d_s2ds(x, w, wds, bits=4, mode="po2", fsr=1, post_scale=None, post_shift=None, act="none",
+                 post_scale_ds=None, post_shift_ds=None):
+    """A stage's stride-2 transition in one launch (po2q_qconv2d_s2ds_f32): the 3x3 stride-2 conv1 and
+    the 1x1 stride-2 projection shortcut of the first BasicBlock (reference resnet.py:55-71, each a
+    QuantizedConv2d.forward, quantized_conv.py:32-38) on the same x, which is read once:
+        y   = act(conv(x, Q(w), stride 2, pad 1) * post_scale + post_shift)
+        yds = conv(x, Q(wds), stride 2) * post_scale_ds + post_shift_ds
+    Returns (y, yds)."""
+    for t, what in ((x, "input"), (w, "weight"), (wds, "shortcut weight")):
+        _require_hip_f32(t, what)
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: qconv2d_s2ds needs the operator library (PO2Q_LIB selects another build)")
+    return _op_call(O.qconv2d_s2ds, x, w, wds, int(bits), MODES[mode], int(fsr), post_scale, post_shift, ACTS[act],
+                    post_scale_ds, post_shift_ds)
 
 
 def conv_wgrad(x, gy, wshape, stride=1, padding=0, dilation=1, groups=1):

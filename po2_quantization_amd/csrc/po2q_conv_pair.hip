@@ -75,7 +75,8 @@ __device__ __forceinline__ int ychunk(int P, int c4) {
 // Conv 1 runs in the transposed MFMA form (A = weights, B = x) so each lane holds 4
 // consecutive channels of one pixel: its epilogue splits them and writes 8 bytes per plane.
 // CC: 16 (7 waves of 32 columns at W = 224, weights in VGPRs) or 32 (7 waves of 16 columns
-// at W = 112; conv 2's B fragments in LDS).  PD: x ring slots.  NTS: non-temporal stores.
+// at W = 112; conv 2's B fragments in LDS).  PD: x ring slots.  NTS bit 0: non-temporal
+// stores, bit 1: non-temporal x loads.
 // E: 0 = plain chain (no bias / affine / activation / residual: y = scale * acc), 1 = the
 // general epilogues (the kernel is bound by vector-instruction issue, so the plain chain
 // skips that work).
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(2 * wave) * 1024u;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            rows_dma16<false>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
+            rows_dma16<(NTS & 2) != 0>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
         if constexpr (RES) {
             const int o = jn - 5;
             const bool ook = jn >= 5 && o < rbe;
@@ -510,6 +511,7 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
     if (pp.C == c && pp.pd == d && pp.nts == nt) return launch_pair_t<c, d, nt>(pp, a, x, y, res, s);
     PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
     PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
+    PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
 #undef PO2Q_PR
     return hipErrorInvalidValue;
 }
@@ -519,15 +521,17 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 // ------------------------------------------------------------------ C ABI --
 namespace {
 
-// variant knob: PO2Q_PAIR_VARIANT = pd * 10 + nts (pd 2 / 3 x ring slots, nts 0 / 1
-// non-temporal stores); default 20
+// variant knob: PO2Q_PAIR_VARIANT = pd * 10 + nts (pd 2 / 3 x ring slots, nts bit 0:
+// non-temporal stores, bit 1 (pd 2 only): non-temporal x loads); default 23: non-temporal
+// loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32 (bs = 256,
+// profiles/r02_pair_nt.log)
 void pair_variant(int& pd, int& nts) {
     pd = 2;
-    nts = 0;
+    nts = 3;
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
         const int v = atoi(e);
         const int d = v / 10, t = v % 10;
-        if ((d == 2 || d == 3) && (t == 0 || t == 1)) {
+        if ((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) {
             pd = d;
             nts = t;
         }
@@ -576,7 +580,7 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // C = 32 (stage 2 @112): 0.366 ms per pair alone but 0.418 ms inside the ResNet56 chain,
     // against 2 x 0.197 ms for the single-conv kernel there (profiles/r02_v7_kernel_stats.csv):
     // the pair is not the faster path, so the advisory says no (the kernel stays callable)
-    if (C == 32) return 0;
+    if (C == 32 && !getenv("PO2Q_PAIR_C32")) return 0;  // PO2Q_PAIR_C32=1: advise it anyway (A/B runs)
     po2q::PairPlan pp;
     int pd, nts;
     pair_variant(pd, nts);

@@ -384,10 +384,9 @@ hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
                                  int act, hipStream_t s, const WQuant& q);
 
-// stride-2 full-row blocks (po2q_conv_rows2.hip: 3x3 s2 16 -> 32, plan vrx = 5)
+// stride-2 full-row blocks (po2q_conv_rows2.hip: 3x3 s2 16 -> 32, plan vrx = 5); launch_conv_rows2
+// is declared in po2q_internal.h
 void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out);
-hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
-                             const float* ps, const float* pb, int act, bool epi, const WQuant& q);
 
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
     const ConvPlan& b = base;

@@ -16,15 +16,23 @@
 //     output t, an odd-offset row adds tap row 2 to output t - 1 (which completes it) and
 //     tap row 0 to output t: two accumulator slots rotate, output rows are stored every
 //     other step (the steps between issue dropped stores, so the vmcnt count holds);
-//   * both weights are quantized + packed by the block into LDS (fused staging): one launch.
+//   * both weights are quantized + packed by the block into LDS (fused staging): one launch;
+//   * DS: the block's 1x1 / stride-2 / pad-0 projection shortcut (layer2.0.downsample.0 /
+//     layer3.0.downsample.0, same C -> 2C) comes from the same x rows: its input pixel
+//     (2t, 2p) is tap (1, 1) of output (t, p), so it is one more k-step of MFMAs on the
+//     fragment the odd-offset row already holds, with its own quantized weight (own scale),
+//     stored to a second output in the odd steps (dropped stores in the even ones).  x is
+//     read once for both convs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <string>
 #include <type_traits>
 #include <vector>
 
+#include "../../include/po2q.h"
 #include "po2q_epi.h"
 #include "po2q_internal.h"
 #include "po2q_quant_dev.h"
@@ -47,9 +55,13 @@ struct Rows2Args {
     const float* pb;
     int act;
     WQuant q;
+    float* yds;        // DS: shortcut output [N, K, P, Q]; yds = Q(wds) * x[::2, ::2] (* psd[k] + pbd[k])
+    WQuant qd;         // DS: the 1x1 weight [K, C, 1, 1]
+    const float* psd;
+    const float* pbd;
 };
 
-template <int CC, int PD, bool EPI, int NTS, int ND>
+template <int CC, int PD, bool EPI, int NTS, int ND, bool DS = false>
 __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x, const float* __restrict__ bias,
                                                      float* __restrict__ y, Rows2Args a) {
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
@@ -63,6 +75,7 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
     uint4* wl = reinterpret_cast<uint4*>(lds);                    // [NF][64] B fragments
     unsigned char* raw = lds + NF * 1024;                         // PD slots [C][W] fp32
     unsigned char* slab = raw + PD * a.rawslot + wave * (3 * PL);  // this wave's planes
+    uint4* wld = reinterpret_cast<uint4*>(raw + PD * a.rawslot + nw * (3 * PL));  // DS: [NT][64]
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -130,7 +143,17 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
 
     const int PQ = a.P * a.Q;
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * K * PQ, K * PQ * 4);
-    constexpr int ST = NT;  // stores per step (every step; odd steps' are dropped)
+    constexpr int ST = DS ? 2 * NT : NT;  // stores per step (every step; the idle output's are dropped)
+    const __amdgpu_buffer_rsrc_t ryd = rows_rsrc(DS ? a.yds + (int64_t)n * K * PQ : y, DS ? K * PQ * 4 : 4);
+    // DS: the k-step of the A fragment that holds tap (., 1) -- O[p]: k-step 0's upper half
+    // (C = 16, the lower half is tap 0: zero rows in the shortcut's B fragment) or k-step 1
+    constexpr int KDS = CC == 16 ? 0 : 1;
+    float scaled = 1.0f;
+    bool find = true;
+    float epsd[NT], epbd[NT];
+    floatx4 accd[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) accd[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     float scale = 1.0f;
     bool fin = true;
@@ -181,6 +204,40 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
         }
     };
 
+    // DS: the shortcut of output row t (local) from the odd-offset row's tap-1 fragment, stored
+    // when `valid` (else NT dropped stores keep the count)
+    auto ds_row = [&](int t, bool valid) __attribute__((always_inline)) {
+        if (valid) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                af[pl] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slab + pl * PL + aoff[KDS]));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const bf16x8 b = __builtin_bit_cast(bf16x8, wld[nt * 64 + lane]);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    accd[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl], b, accd[nt], 0, 0, 0);
+            }
+        }
+        const bool orow = valid && t >= 0 && t < rbe;
+        const int q = q0 + 4 * (lane >> 4);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int k = 16 * nt + (lane & 15);
+            floatx4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float u = accd[nt][e] * scaled;
+                if constexpr (EPI) u = u * epsd[nt] + epbd[nt];
+                v[e] = u;
+            }
+            const uint32_t yo = (uint32_t)k * (uint32_t)PQ + (uint32_t)(orow ? p0 + t : 0) * a.Q + (uint32_t)q;
+            rows_store<(NTS & 1) != 0>(ryd, (orow && q < a.Q) ? yo * 4u : 0x7fffffffu, v);
+            if (valid) accd[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
     // vm ops after this wave's DMAs of row j (issued in step j - PD + 1, after its barrier)
     // until the wait of step j: that step's ST stores, then ND DMAs + ST stores per step
     constexpr int VMW = ST + (PD - 2) * (ND + ST);
@@ -226,10 +283,12 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
             mfmas(std::integral_constant<int, 2>{}, std::integral_constant<int, PREV>{});
             mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, CUR>{});
             store_row(std::integral_constant<int, PREV>{}, t - 1, true);
+            if constexpr (DS) ds_row(t, false);  // dropped: keeps the count
         } else {
             constexpr int CUR = (S4 >> 1) & 1;
             mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, CUR>{});
             store_row(std::integral_constant<int, CUR>{}, t, false);  // dropped: keeps the count
+            if constexpr (DS) ds_row(t, true);   // input row 2 (p0 + t): the shortcut of output t
         }
     };
 
@@ -249,6 +308,28 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
         scale = wq_prologue(a.q, thr, red, nw, fin);
         __syncthreads();  // every wave's scratch reads done before wl (disjoint) -- and thr stays
         for (int e = tid; e < NF * 64; e += blockDim.x) wl[e] = wq_frag_rows(a.q, CC, K, CC, NT, KS, e, scale, fin, thr);
+        if constexpr (DS) {
+            __syncthreads();  // thr / red reads of the 3x3 weight done
+            scaled = wq_prologue(a.qd, thr, red, nw, find);
+            for (int e = tid; e < NT * 64; e += blockDim.x) {
+                // B fragment of k-step KDS: rows k = 8 g .. 8 g + 7 (g = lane >> 4) are tap 1's
+                // channels (C = 32: c = 8 g + i; C = 16: g >= 2, c = 8 (g & 1) + i; else zero)
+                const int l = e & 63, nt = e >> 6, g = l >> 4, k = 16 * nt + (l & 15);
+                const bool ok = CC == 32 || g >= 2;
+                const int c0 = CC == 32 ? 8 * g : 8 * (g & 1);
+                uint32_t h[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    h[i] = ok ? pack_one(a.qd.w[k * CC + c0 + i], scaled, find, a.qd.mode, a.qd.lo, a.qd.hi, thr) : 0u;
+                wld[e] = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int k = 16 * nt + (lane & 15);
+                epsd[nt] = (EPI && a.psd) ? a.psd[k] : 1.0f;
+                epbd[nt] = (EPI && a.pbd) ? a.pbd[k] : 0.0f;
+            }
+        }
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int k = 16 * nt + (lane & 15);
@@ -259,6 +340,10 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(bk[nt]), "+v"(eps_[nt]), "+v"(epb_[nt]));
+        if constexpr (DS) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(epsd[nt]), "+v"(epbd[nt]));
+        }
         __syncthreads();  // wl complete, scratch free
         if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + ZOFF) = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -342,8 +427,12 @@ void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
 template <int CC, int PD, bool EPI, int NTS, int ND>
 static hipError_t launch_rows2_nd(const ConvPlan& p, const Rows2Args& a, const float* x, const float* bias, float* y,
                                   hipStream_t s) {
-    hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND>), dim3((unsigned)p.blocks), dim3(64 * (p.TQ / 16)),
-                       p.lds_bytes, s, x, bias, y, a);
+    if (a.yds)
+        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND, true>), dim3((unsigned)p.blocks), dim3(64 * (p.TQ / 16)),
+                           p.lds_bytes + (size_t)(2 * CC / 16) * 1024, s, x, bias, y, a);
+    else
+        hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND>), dim3((unsigned)p.blocks), dim3(64 * (p.TQ / 16)),
+                           p.lds_bytes, s, x, bias, y, a);
     return hipGetLastError();
 }
 
@@ -361,9 +450,11 @@ static hipError_t launch_rows2_t(const ConvPlan& p, const Rows2Args& a, const fl
 }
 
 hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
-                             const float* ps, const float* pb, int act, bool epi, const WQuant& q) {
+                             const float* ps, const float* pb, int act, bool epi, const WQuant& q, float* yds,
+                             const WQuant& qd, const float* psd, const float* pbd) {
     if (p.kind != KIND_BF16X3_ROWS || p.vrx != 5 || !q.w || !((p.C == 16 && p.K == 32) || (p.C == 32 && p.K == 64)))
         return hipErrorInvalidValue;
+    if (yds && (!qd.w || p.lds_bytes + (size_t)(p.K / 16) * 1024 > 160 * 1024)) return hipErrorInvalidValue;
     Rows2Args a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP; a.nseg = p.tilesP; a.items = p.N * p.tilesP;
@@ -371,6 +462,7 @@ hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bia
     a.rawslot = p.dma_nck;
     a.ps = ps; a.pb = pb; a.act = act;
     a.q = q;
+    a.yds = yds; a.qd = qd; a.psd = psd; a.pbd = pbd;
 #define PO2Q_R2(d, e, nt) \
     if (p.C == 16 && p.pd == d && epi == e && p.nts == nt) return launch_rows2_t<16, d, e, nt>(p, a, x, bias, y, s);
     PO2Q_R2(2, false, 0) PO2Q_R2(2, false, 1) PO2Q_R2(4, false, 0) PO2Q_R2(4, false, 1)
@@ -382,3 +474,80 @@ hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bia
 }
 
 }  // namespace po2q
+
+// ------------------------------------------------------------------ C ABI --
+namespace {
+
+// The stride-2 plan for the fused conv + shortcut: the plan the sweeps measured fastest
+// (profiles/r02_stage_s2*_sweep.jsonl: C = 16 ring depth 4, C = 32 depth 2; whole-image
+// segments at bs >= 256), else the first stride-2 candidate.
+bool s2ds_plan(po2q::ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
+    if (N <= 0 || H <= 0 || W <= 0 || !((C == 16) || (C == 32))) return false;
+    if (mode != PO2Q_MODE_PO2 && mode != PO2Q_MODE_PO2_PLUS) return false;
+    std::vector<po2q::ConvPlan> cands;
+    if (!po2q::plan_candidates(cands, N, C, H, W, 2 * C, 3, 3, 2, 2, 1, 1, 1, 1, 1, mode, bits, fsr, PO2Q_PREC_BF16X3))
+        return false;
+    const int want = C == 16 ? 4 : 2;
+    int pick = -1;
+    for (int i = 0; i < (int)cands.size(); ++i) {
+        const po2q::ConvPlan& c = cands[i];
+        if (c.kind != po2q::KIND_BF16X3_ROWS || c.vrx != 5 || c.nts != 0) continue;
+        if (c.lds_bytes + (size_t)(2 * C / 16) * 1024 > 160 * 1024) continue;
+        if (pick < 0 || (c.pd == want && cands[pick].pd != want)) pick = i;
+    }
+    if (pick < 0) return false;
+    p = cands[pick];
+    return true;
+}
+
+}  // namespace
+
+int po2q_qconv2d_s2ds_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
+    po2q::ConvPlan p;
+    return s2ds_plan(p, N, C, H, W, bits, fsr, mode) ? 1 : 0;
+}
+
+int po2q_qconv2d_s2ds_f32(const float* x, const float* w, const float* wds, float* y, float* yds, int64_t N,
+                          int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode, const float* post_scale,
+                          const float* post_shift, int act, const float* post_scale_ds, const float* post_shift_ds,
+                          void* stream) {
+    if (!x || !w || !wds || !y || !yds) {
+        po2q::set_error("po2q: s2ds: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (bits < 1 || bits > 16) {
+        po2q::set_error("po2q: bits must be in [1, 16]");
+        return PO2Q_ERR_INVALID;
+    }
+    if (act < PO2Q_ACT_NONE || act > PO2Q_ACT_SILU) {
+        po2q::set_error("po2q: unknown activation");
+        return PO2Q_ERR_INVALID;
+    }
+    if (y == yds || x == y || x == yds) {
+        po2q::set_error("po2q: s2ds: y, yds and x must not alias");
+        return PO2Q_ERR_INVALID;
+    }
+    po2q::ConvPlan p;
+    if (!s2ds_plan(p, N, C, H, W, bits, fsr, mode)) {
+        po2q::set_error("po2q: s2ds: 3x3 stride-2 C -> 2C with C = 16 or 32 and a po2 / po2+ weight only");
+        return PO2Q_ERR_UNSUPPORTED;
+    }
+    po2q::WQuant q, qd;
+    q.w = w;
+    q.n = (int)(2 * C * C * 9);
+    q.lo = fsr - (1 << (bits - 1));
+    q.hi = fsr - 1;
+    q.mode = mode - 1;
+    qd = q;
+    qd.w = wds;
+    qd.n = (int)(2 * C * C);
+    const bool epi = post_scale || post_shift || act != PO2Q_ACT_NONE || post_scale_ds || post_shift_ds;
+    const hipError_t e = po2q::launch_conv_rows2(p, x, nullptr, y, reinterpret_cast<hipStream_t>(stream), post_scale,
+                                                 post_shift, act, epi, q, yds, qd, post_scale_ds, post_shift_ds);
+    if (e != hipSuccess) {
+        po2q::set_error(std::string("po2q: s2ds launch: ") + hipGetErrorString(e));
+        return PO2Q_ERR_HIP;
+    }
+    return PO2Q_OK;
+}
+

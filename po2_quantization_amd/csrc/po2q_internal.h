@@ -80,6 +80,14 @@ struct WQuant {
     int mode = 0;              // 0 po2, 1 po2+ (threshold row)
 };
 
+// Stride-2 full-row kernel (po2q_conv_rows2.hip: 3x3 s2 C -> 2C, plan vrx = 5, fused staging).
+// yds != NULL: the same launch also computes the block's 1x1 stride-2 shortcut with the weight
+// qd into yds ([N, K, P, Q]; epilogue psd / pbd when epi), reading x once for both convs.
+hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bias, float* y, hipStream_t s,
+                             const float* ps, const float* pb, int act, bool epi, const WQuant& q,
+                             float* yds = nullptr, const WQuant& qd = WQuant{}, const float* psd = nullptr,
+                             const float* pbd = nullptr);
+
 struct PlanCand {
     double cost;  // planner heuristic, lower is better
     ConvPlan plan;

@@ -11,6 +11,7 @@
 //   po2q::qconv2d_fused  the same + eval BatchNorm affine, residual add and activation of
 //                        the blocks (resnet.py:55-71, mobilenet.py:32-33, mobile_vit.py:20-21)
 //   po2q::qconv2d_pair   two chained 16-channel 3x3 qconvs (+ BN / act between and after, residual)
+//   po2q::qconv2d_s2ds   a stage's 3x3 stride-2 conv1 + 1x1 stride-2 shortcut on one read of x
 //                        in one launch: a ResNet56 stage-1 BasicBlock (resnet.py:55-71)
 //   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
 //                        STE, utils/quantizers.py:34-36)
@@ -311,6 +312,53 @@ at::Tensor qconv2d_pair_meta(const at::Tensor& x, const at::Tensor&, const at::T
     return at::empty_like(x);
 }
 
+// A stage's stride-2 3x3 conv and its 1x1 stride-2 shortcut in one launch (po2q_qconv2d_s2ds_f32)
+std::tuple<at::Tensor, at::Tensor> qconv2d_s2ds(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& wds_,
+                                                int64_t bits, int64_t mode, int64_t fsr,
+                                                const c10::optional<at::Tensor>& ps, const c10::optional<at::Tensor>& pb,
+                                                int64_t act, const c10::optional<at::Tensor>& psd,
+                                                const c10::optional<at::Tensor>& pbd) {
+    check_hip_f32(x_, "input");
+    check_hip_f32(w_, "weight");
+    check_hip_f32(wds_, "shortcut weight");
+    TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && wds_.dim() == 4, "po2q: s2ds: 4-D input and weights");
+    const int64_t C = x_.size(1), K = 2 * C;
+    TORCH_CHECK(w_.size(0) == K && w_.size(1) == C && w_.size(2) == 3 && w_.size(3) == 3,
+                "po2q: s2ds: weight must be [2C, C, 3, 3]");
+    TORCH_CHECK(wds_.size(0) == K && wds_.size(1) == C && wds_.size(2) == 1 && wds_.size(3) == 1,
+                "po2q: s2ds: shortcut weight must be [2C, C, 1, 1]");
+    TORCH_CHECK(w_.device() == x_.device() && wds_.device() == x_.device(), "po2q: s2ds: tensors on one device");
+    for (auto [t, what] : {std::make_pair(&ps, "post_scale"), std::make_pair(&pb, "post_shift"),
+                           std::make_pair(&psd, "post_scale_ds"), std::make_pair(&pbd, "post_shift_ds")})
+        check_vec(*t, x_, K, what);
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous(), w = w_.contiguous(), wds = wds_.contiguous();
+    auto cont = [](const c10::optional<at::Tensor>& t) -> c10::optional<at::Tensor> {
+        return t.has_value() ? c10::optional<at::Tensor>(t->contiguous()) : c10::nullopt;
+    };
+    const auto s1 = cont(ps), t1 = cont(pb), s2 = cont(psd), t2 = cont(pbd);
+    const int64_t P = (x.size(2) - 1) / 2 + 1, Q = (x.size(3) - 1) / 2 + 1;
+    at::Tensor y = at::empty({x.size(0), K, P, Q}, x.options());
+    at::Tensor yds = at::empty({x.size(0), K, P, Q}, x.options());
+    if (x.size(0) == 0) return {y, yds};
+    const int st = po2q_qconv2d_s2ds_f32(x.data_ptr<float>(), w.data_ptr<float>(), wds.data_ptr<float>(),
+                                         y.data_ptr<float>(), yds.data_ptr<float>(), x.size(0), C, x.size(2),
+                                         x.size(3), (int)bits, (int)fsr, (int)mode, opt_ptr(s1), opt_ptr(t1), (int)act,
+                                         opt_ptr(s2), opt_ptr(t2), stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return {y, yds};
+}
+
+std::tuple<at::Tensor, at::Tensor> qconv2d_s2ds_meta(const at::Tensor& x, const at::Tensor&, const at::Tensor&,
+                                                     int64_t, int64_t, int64_t, const c10::optional<at::Tensor>&,
+                                                     const c10::optional<at::Tensor>&, int64_t,
+                                                     const c10::optional<at::Tensor>&,
+                                                     const c10::optional<at::Tensor>&) {
+    const int64_t P = (x.size(2) - 1) / 2 + 1, Q = (x.size(3) - 1) / 2 + 1;
+    return {at::empty({x.size(0), 2 * x.size(1), P, Q}, x.options()),
+            at::empty({x.size(0), 2 * x.size(1), P, Q}, x.options())};
+}
+
 // ---- Meta (shape-only) implementations ------------------------------------------
 at::Tensor qconv2d_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                         at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation, int64_t groups,
@@ -353,6 +401,9 @@ TORCH_LIBRARY(po2q, m) {
     m.def("qconv2d_pair(Tensor x, Tensor w1, Tensor w2, int bits, int mode, int fsr=1, Tensor? bias1=None, "
           "Tensor? bias2=None, Tensor? post_scale1=None, Tensor? post_shift1=None, int act1=0, "
           "Tensor? post_scale2=None, Tensor? post_shift2=None, Tensor? residual=None, int act2=0) -> Tensor");
+    m.def("qconv2d_s2ds(Tensor x, Tensor w, Tensor wds, int bits, int mode, int fsr=1, Tensor? post_scale=None, "
+          "Tensor? post_shift=None, int act=0, Tensor? post_scale_ds=None, Tensor? post_shift_ds=None) "
+          "-> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
@@ -362,6 +413,7 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("qconv2d_fused", &qconv2d_fused);
     m.impl("conv_wgrad", &conv_wgrad);
     m.impl("qconv2d_pair", &qconv2d_pair);
+    m.impl("qconv2d_s2ds", &qconv2d_s2ds);
 }
 
 TORCH_LIBRARY_IMPL(po2q, Meta, m) {
@@ -371,4 +423,5 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("qconv2d_fused", &qconv2d_fused_meta);
     m.impl("conv_wgrad", &conv_wgrad_meta);
     m.impl("qconv2d_pair", &qconv2d_pair_meta);
+    m.impl("qconv2d_s2ds", &qconv2d_s2ds_meta);
 }

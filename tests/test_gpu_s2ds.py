@@ -1,0 +1,90 @@
+"""GPU parity of the fused stride-2 transition (po2q_qconv2d_s2ds_f32): a stage's first-block
+conv1 (QuantizedConv2d 3x3 stride 2, C -> 2C) and its projection shortcut downsample.0
+(QuantizedConv2d 1x1 stride 2) on the same x in one launch (reference models/resnet.py:55-71,
+each conv QuantizedConv2d.forward, models/quantized_conv.py:32-38), against torch fp32 convs of
+the bit-exact Q(w) (a plain PyTorch fp32 reference) and against the single-conv path.
+Bar: normwise 1e-5 (CONV_TOL)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from po2_quantization_amd import _lib
+from tests._util import CONV_TOL
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def nerr(y, ref):
+    return ((y - ref).abs().max() / ref.abs().max()).item()
+
+
+def make(N, C, H, W, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    w = (torch.randn(2 * C, C, 3, 3, generator=g) * 0.1).to(DEV)
+    wds = (torch.randn(2 * C, C, 1, 1, generator=g) * 0.2).to(DEV)
+    return x, w, wds
+
+
+SHAPES = [(2, 16, 40, 40), (1, 16, 9, 64), (1, 16, 17, 8), (2, 16, 30, 224), (3, 16, 2, 16),
+          (2, 32, 40, 40), (1, 32, 17, 8), (2, 32, 30, 112), (1, 32, 1, 16)]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+"])
+def test_s2ds_vs_torch(shape, mode):
+    N, C, H, W = shape
+    x, w, wds = make(N, C, H, W, hash(shape) & 0xFFFF)
+    assert _lib.s2ds_supported(x.shape, 4, mode)
+    y, yds = _lib.qconv2d_s2ds(x, w, wds, 4, mode)
+    ref = F.conv2d(x, _lib.quantize(w, 4, mode), None, 2, 1)
+    refds = F.conv2d(x, _lib.quantize(wds, 4, mode), None, 2, 0)
+    assert y.shape == ref.shape and yds.shape == refds.shape
+    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+    assert nerr(yds, refds) <= CONV_TOL, nerr(yds, refds)
+    # the 3x3 output is the single-conv stride-2 kernel's, same bf16x3 arithmetic
+    y1 = _lib.qconv2d(x, w, None, 2, 1, 1, 1, 4, mode)
+    assert nerr(y, y1) <= 1e-6, nerr(y, y1)
+
+
+@pytest.mark.parametrize("C", [16, 32])
+def test_s2ds_epilogues_vs_torch(C):
+    """Eval BatchNorm + ReLU on conv1, eval BatchNorm on the shortcut (BasicBlock's two branches)."""
+    x, w, wds = make(2, C, 36, 64, 7 + C)
+    g = torch.Generator().manual_seed(3)
+    ps, psd = (torch.rand(2 * C, generator=g) + 0.5).to(DEV), (torch.rand(2 * C, generator=g) + 0.5).to(DEV)
+    pb, pbd = (torch.randn(2 * C, generator=g) * 0.1).to(DEV), (torch.randn(2 * C, generator=g) * 0.1).to(DEV)
+    y, yds = _lib.qconv2d_s2ds(x, w, wds, 4, "po2+", post_scale=ps, post_shift=pb, act="relu",
+                               post_scale_ds=psd, post_shift_ds=pbd)
+    v = lambda t: t.view(1, -1, 1, 1)  # noqa: E731
+    ref = torch.relu(F.conv2d(x, _lib.quantize(w, 4, "po2+"), None, 2, 1) * v(ps) + v(pb))
+    refds = F.conv2d(x, _lib.quantize(wds, 4, "po2+"), None, 2, 0) * v(psd) + v(pbd)
+    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+    assert nerr(yds, refds) <= CONV_TOL, nerr(yds, refds)
+
+
+@pytest.mark.parametrize("C,H", [(16, 224), (32, 112)])
+def test_s2ds_full_size(C, H):
+    """BASELINE size (bs = 256): layer2.0 (16 -> 32 @224) and layer3.0 (32 -> 64 @112)."""
+    torch.manual_seed(0)
+    x = torch.relu(torch.randn(256, C, H, H, device=DEV))
+    w = torch.randn(2 * C, C, 3, 3, device=DEV) * 0.1
+    wds = torch.randn(2 * C, C, 1, 1, device=DEV) * 0.2
+    y, yds = _lib.qconv2d_s2ds(x, w, wds, 4, "po2")
+    ref = F.conv2d(x, _lib.quantize(w, 4, "po2"), None, 2, 1)
+    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+    del ref
+    refds = F.conv2d(x, _lib.quantize(wds, 4, "po2"), None, 2, 0)
+    assert nerr(yds, refds) <= CONV_TOL, nerr(yds, refds)
+
+
+def test_s2ds_rejects():
+    assert not _lib.s2ds_supported((2, 64, 56, 56))
+    assert not _lib.s2ds_supported((2, 16, 40, 42))  # W % 4
+    x = torch.randn(1, 64, 8, 8, device=DEV)
+    with pytest.raises(_lib.Po2qError):
+        _lib.qconv2d_s2ds(x, torch.randn(128, 64, 3, 3, device=DEV), torch.randn(128, 64, 1, 1, device=DEV))
+    x = torch.randn(1, 16, 8, 8, device=DEV)
+    with pytest.raises(_lib.Po2qError, match="shortcut weight"):
+        _lib.qconv2d_s2ds(x, torch.randn(32, 16, 3, 3, device=DEV), torch.randn(32, 16, 3, 3, device=DEV))

@@ -32,3 +32,14 @@ def test_cpu_tensors_have_no_kernel():
     O = _lib.ops()
     with pytest.raises(RuntimeError):
         O.qconv2d(torch.randn(1, 4, 8, 8), torch.randn(4, 4, 3, 3), None, [1, 1], [1, 1], [1, 1], 1, 4, 1)
+
+
+@pytest.mark.parametrize("C,H,W", [(16, 224, 224), (32, 112, 112), (16, 17, 8)])
+def test_s2ds_meta_shapes_match_both_convs(C, H, W):
+    """qconv2d_s2ds: the 3x3 s2 p1 conv and the 1x1 s2 conv of the same x have one output shape."""
+    x = torch.empty(2, C, H, W, device="meta")
+    w = torch.empty(2 * C, C, 3, 3, device="meta")
+    wds = torch.empty(2 * C, C, 1, 1, device="meta")
+    y, yds = _lib.ops().qconv2d_s2ds(x, w, wds, 4, 1)
+    assert y.shape == torch.nn.functional.conv2d(x, w, None, 2, 1).shape
+    assert yds.shape == torch.nn.functional.conv2d(x, wds, None, 2, 0).shape
