@@ -47,6 +47,15 @@ class BasicBlock(nn.Module):
                 return _lib.qconv2d_pair(x, self.conv1.weight, self.conv2.weight, self.conv1.bits,
                                          NATIVE_MODES[self.conv1.quantize_fn], post_scale1=ps1, post_shift1=pb1,
                                          act1="relu", post_scale2=ps2, post_shift2=pb2, residual=x, act2="relu")
+            if self._s2ds_ok(x):
+                # conv1 -> bn1 -> relu and downsample (1x1 conv -> bn) on ONE read of x
+                # (po2q_qconv2d_s2ds_f32), then conv2 -> bn2 -> + shortcut -> relu
+                ps1, pb1 = fold_bn(self.bn1)
+                psd, pbd = fold_bn(self.downsample[1])
+                out, shortcut = _lib.qconv2d_s2ds(x, self.conv1.weight, self.downsample[0].weight, self.conv1.bits,
+                                                  NATIVE_MODES[self.conv1.quantize_fn], post_scale=ps1,
+                                                  post_shift=pb1, act="relu", post_scale_ds=psd, post_shift_ds=pbd)
+                return self.conv2.fused(out, bn=self.bn2, residual=shortcut, act="relu")
             shortcut = x if self.downsample is None else run_fused_sequence(self.downsample, x)
             out = self.conv1.fused(x, bn=self.bn1, act="relu")
             return self.conv2.fused(out, bn=self.bn2, residual=shortcut, act="relu")
@@ -67,6 +76,25 @@ class BasicBlock(nn.Module):
                 and c2.precision != "fp32" and c1.bias is None and c2.bias is None
                 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
                 and _lib.pair_supported(x.shape, c1.bits, mode))
+
+    def _s2ds_ok(self, x):
+        """conv1 (3x3 stride 2, C -> 2C) and the projection shortcut (QuantizedConv2d 1x1 stride 2 +
+        BatchNorm, models/resnet.py:100-105) eligible for the fused stride-2 kernel: same native PO2
+        quantizer and bits, bf16x3 arithmetic allowed, no biases."""
+        c1, ds = self.conv1, self.downsample
+        if ds is None or len(ds) != 2 or not isinstance(ds[0], QuantizedConv2d):
+            return False
+        d = ds[0]
+        mode = NATIVE_MODES.get(c1.quantize_fn)
+        return (mode in ("po2", "po2+") and d.quantize_fn is c1.quantize_fn and d.bits == c1.bits
+                and c1.in_channels in (16, 32) and c1.out_channels == 2 * c1.in_channels
+                and tuple(c1.stride) == (2, 2) and tuple(c1.padding) == (1, 1) and tuple(c1.dilation) == (1, 1)
+                and d.in_channels == c1.in_channels and d.out_channels == c1.out_channels
+                and tuple(d.kernel_size) == (1, 1) and tuple(d.stride) == (2, 2) and tuple(d.padding) == (0, 0)
+                and c1.groups == 1 and d.groups == 1 and c1.bias is None and d.bias is None
+                and c1.precision != "fp32" and d.precision != "fp32"
+                and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and _lib.s2ds_supported(x.shape, c1.bits, mode))
 
     def get_quantization_error(self):
         e1, n1 = self.conv1.get_quantization_error()

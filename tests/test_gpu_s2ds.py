@@ -88,3 +88,30 @@ def test_s2ds_rejects():
     x = torch.randn(1, 16, 8, 8, device=DEV)
     with pytest.raises(_lib.Po2qError, match="shortcut weight"):
         _lib.qconv2d_s2ds(x, torch.randn(32, 16, 3, 3, device=DEV), torch.randn(32, 16, 3, 3, device=DEV))
+
+
+@pytest.mark.parametrize("stage,C,H", [(2, 16, 56), (3, 32, 32)])
+@pytest.mark.parametrize("q", ["po2", "po2+"])
+def test_basicblock_eval_fused_equals_module_sequence(stage, C, H, q, monkeypatch):
+    """ResNet56 layer{2,3}.0 in eval: BasicBlock.forward through qconv2d_s2ds (conv1 + BN + ReLU and
+    the 1x1 shortcut + BN on one read of x) equals the plain module sequence."""
+    from po2_quantization_amd.models import quantized_conv as qc
+    from po2_quantization_amd.models.model import get_model
+    from po2_quantization_amd.utils.quantizers import quantizer_dict
+
+    m = get_model("resnet56", 10, quantizer_dict[q], 4, (32, 32))
+    blk = getattr(m, "layer%d" % stage)[0]
+    g = torch.Generator().manual_seed(stage)
+    for bn in (blk.bn1, blk.bn2, blk.downsample[1]):
+        bn.running_mean.copy_(torch.randn(bn.num_features, generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(bn.num_features, generator=g) + 0.5)
+        bn.weight.data.copy_(torch.rand(bn.num_features, generator=g) + 0.5)
+        bn.bias.data.copy_(torch.randn(bn.num_features, generator=g) * 0.1)
+    blk = blk.to(DEV).eval()
+    x = torch.relu(torch.randn(4, C, H, H, generator=g)).to(DEV)
+    assert blk._s2ds_ok(x)
+    with torch.no_grad():
+        y = blk(x)
+        monkeypatch.setattr(qc, "INFERENCE_FUSION", False)
+        ref = blk(x)
+    assert nerr(y, ref) <= 1e-6, nerr(y, ref)
