@@ -76,9 +76,16 @@ class QConvChain:
         self.events = []
         self.pair = True             # conv1 -> conv2 of stage-1 / stage-2 blocks as one pair launch
         self.s2ds = True             # stride-2 conv1 + its 1x1 shortcut of a stage's first block as one launch
+        self.packed = None           # _lib.PackedConvs: the single-conv layers' weight packs as one batched launch
+        self.packed_idx = {}         # layer index -> PackedConvs index
+        self.shapes = {}             # layer index -> input shape (recorded by conv())
 
-    def conv(self, i, x):
+    def conv(self, i, x, direct=False):
         _, C, K, R, st, pad, _ = self.layers[i]
+        j = None if direct else self.packed_idx.get(i)
+        if j is not None:
+            return self.packed.conv(j, x)
+        self.shapes[i] = tuple(x.shape)
         return _lib.qconv2d(x, self.weights[i], None, st, pad, 1, 1, self.bits, self.mode, 1, self.precision)
 
     def pairable(self, i, x):
@@ -89,7 +96,18 @@ class QConvChain:
         return C1 in (16, 32) and (K1, C2, K2, R1, R2, s1, s2) == (C1, C1, C1, 3, 3, 1, 1) \
             and self.mode in ("po2", "po2+") and _lib.pair_supported(x.shape, self.bits, self.mode)
 
+    def enable_packed(self):
+        """After a (autotuning) forward: every layer that ran as a single-conv launch gets its
+        weight quantize + pack from one batched launch at the start of each forward
+        (_lib.PackedConvs: po2q_qconv2d_plan_pack_batch), then its conv from the packed workspace."""
+        idx = sorted(self.shapes)
+        specs = [(self.shapes[i], self.weights[i], self.layers[i][4], self.layers[i][5]) for i in idx]
+        self.packed = _lib.PackedConvs(specs, self.bits, self.mode)
+        self.packed_idx = {i: j for j, i in enumerate(idx)}
+
     def forward(self, x, record=False):
+        if self.packed is not None:
+            self.packed.pack()  # every single-conv layer's weight, quantized + packed in one launch
         i = 0
         while i < len(self.layers):
             name, _, _, _, _, _, role = self.layers[i]
@@ -260,6 +278,8 @@ def main():
                     help="run every conv as its own launch (no stage-1 conv1->conv2 pair kernel)")
     ap.add_argument("--no-s2ds", action="store_true",
                     help="run a stage's stride-2 conv1 and its 1x1 shortcut as two launches (each reads x)")
+    ap.add_argument("--no-pack-batch", action="store_true",
+                    help="quantize + pack each single-conv layer's weight in its own launch")
     ap.add_argument("--no-autotune", action="store_true",
                     help="use the heuristic plans instead of autotuning each conv shape on first use")
     args = ap.parse_args()
@@ -292,6 +312,13 @@ def main():
 
     def step(record=False):
         return gather_logits(chain.forward(x, record), gathered, world)
+
+    pack_batch = not args.no_pack_batch and args.quantizer in ("po2", "po2+") and args.precision != "fp32"
+    if pack_batch:
+        with torch.no_grad():  # one untimed forward: autotunes every shape and records the layers' inputs
+            step()
+            torch.cuda.synchronize()
+        chain.enable_packed()
 
     graph = None
     if args.graph:
@@ -349,7 +376,7 @@ def main():
 
     if graph is not None:
         avg_ms = launch_avg_ms((lambda: chain.pair_call(0, xl)) if pair_used else
-                               (lambda: chain.conv(chain.timed_layer, xl)))
+                               (lambda: chain.conv(chain.timed_layer, xl, direct=True)))
     else:
         ev_ms = [a.elapsed_time(b) for a, b in chain.events]
         avg_ms = sum(ev_ms) / max(len(ev_ms), 1)
@@ -393,7 +420,7 @@ def main():
                                % (args.quantizer, Hs, Hs, B),
                      "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(pbytes), "flops": int(pflops)})
         # the single-layer kernel of the same shape (used wherever pairs do not apply)
-        lms = launch_avg_ms(lambda: chain.conv(chain.timed_layer, xl))
+        lms = launch_avg_ms(lambda: chain.conv(chain.timed_layer, xl, direct=True))
         layer_roof = roofline(flops, nbytes, lms)
         layer_roof["traffic"] = traffic_of(plan)
         layer_roof.update({"kernel": layer_kernel, "avg_launch_ms": round(lms, 4), "algorithmic_bytes": int(nbytes),
@@ -411,14 +438,17 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
-        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s%s"
+        "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s%s%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
                                   " (stage-1 conv1->conv2 pairs as one launch each)" if pair_used else "",
                                   " (stride-2 conv1 + 1x1 shortcut of stages 2-3 as one launch each)"
                                   if s2ds_used else "",
+                                  " (weight packs of the single-conv layers batched: one launch per 16)"
+                                  if chain.packed is not None else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "conv_pairs": pair_used,
                    "s2ds": s2ds_used,
+                   "pack_batch": chain.packed is not None,
                    "autotune": _lib.benchmark,
                    "image": Hs, "batch_per_gpu": B, "global_batch": world * B, "quantizer": args.quantizer,
                    "bits": args.bits, "precision": prec, "parallelism": "dp%d" % world, "world_size": world,

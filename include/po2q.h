@@ -285,6 +285,22 @@ int po2q_qconv2d_plan_run(const po2q_conv_plan* plan, const float* x, const floa
 int po2q_qconv2d_plan_describe(const po2q_conv_plan* plan, char* buf, size_t len);
 void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan);
 
+/*
+ * The per-layer weight quantize + pack of a whole forward in one go (each layer's
+ * QuantizedConv2d.forward quantizes its weight, models/quantized_conv.py:32-38): for every
+ * plans[i] whose kernel does not stage its weight itself, quantize + pack w[i] into
+ * workspace[i] (>= po2q_qconv2d_plan_workspace_bytes) -- the bf16x3 packs in
+ * ceil(n / 16) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
+ * from that workspace (w is read only by plans that stage their weight in-kernel); on one
+ * stream the pair equals po2q_qconv2d_plan_run bit for bit.
+ */
+int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, const float* const* w,
+                                 void* const* workspace, const size_t* workspace_bytes, void* stream);
+int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias,
+                                 float* y, const float* post_scale, const float* post_shift,
+                                 const float* residual, int act, const void* workspace,
+                                 size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

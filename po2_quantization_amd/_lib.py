@@ -55,6 +55,8 @@ EXPORTS = (
     "po2q_qconv2d_pair_f32",
     "po2q_qconv2d_s2ds_supported",
     "po2q_qconv2d_s2ds_f32",
+    "po2q_qconv2d_plan_pack_batch",
+    "po2q_qconv2d_plan_run_packed",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -145,6 +147,17 @@ def load():
     L.po2q_qconv2d_pair_supported.argtypes = [i64] * 4 + [i32] * 3
     L.po2q_qconv2d_s2ds_supported.restype = i32
     L.po2q_qconv2d_s2ds_supported.argtypes = [i64] * 4 + [i32] * 3
+    L.po2q_qconv2d_plan_create.restype = i32
+    L.po2q_qconv2d_plan_create.argtypes = [ctypes.POINTER(p), i32] + [i64] * 14 + [i32] * 4
+    L.po2q_qconv2d_plan_workspace_bytes.restype = sz
+    L.po2q_qconv2d_plan_workspace_bytes.argtypes = [p]
+    L.po2q_qconv2d_plan_destroy.restype = None
+    L.po2q_qconv2d_plan_destroy.argtypes = [p]
+    L.po2q_qconv2d_plan_pack_batch.restype = i32
+    L.po2q_qconv2d_plan_pack_batch.argtypes = [i32, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p),
+                                               ctypes.POINTER(sz), p]
+    L.po2q_qconv2d_plan_run_packed.restype = i32
+    L.po2q_qconv2d_plan_run_packed.argtypes = [p] * 8 + [i32, p, sz, p]
     _lib = L
     return L
 
@@ -444,6 +457,70 @@ def qconv2d_pair(x, w1, w2, bits=4, mode="po2", fsr=1, bias1=None, bias2=None, p
         raise Po2qError("po2q: qconv2d_pair needs the operator library (PO2Q_LIB selects another build)")
     return _op_call(O.qconv2d_pair, x, w1, w2, int(bits), MODES[mode], int(fsr), bias1, bias2, post_scale1,
                     post_shift1, ACTS[act1], post_scale2, post_shift2, residual, ACTS[act2])
+
+
+class PackedConvs:
+    """Several QuantizedConv2d forwards (models/quantized_conv.py:32-38) with their weight
+    quantize + pack as ONE batched launch (po2q_qconv2d_plan_pack_batch) and each conv from its
+    packed workspace (po2q_qconv2d_plan_run_packed) -- the same kernels and results as
+    qconv2d() layer by layer, with ceil(n / 16) pack launches instead of one per layer.
+
+    specs: [(x_shape, w, stride, padding)] in call order (groups 1, dilation 1, no bias); the
+    plans are resolved once here, so create it after the shapes were autotuned.  Call pack()
+    once per forward (after any weight update), then conv(i, x) for each layer."""
+
+    def __init__(self, specs, bits=4, mode="po2", fsr=1):
+        L = load()
+        self._L = L
+        self.bits, self.mode, self.fsr = int(bits), MODES[mode], int(fsr)
+        self.plans, self.ws, self.w, self.xshape, self.yshape = [], [], [], [], []
+        for x_shape, w, stride, padding in specs:
+            _require_hip_f32(w, "weight")
+            N, C, H, W = (int(v) for v in x_shape)
+            K, _, R, S = w.shape
+            sh, sw = _pair(stride)
+            ph, pw = _pair(padding)
+            args = (N, C, H, W, K, R, S, sh, sw, ph, pw, 1, 1, 1)
+            key = args + (self.bits, self.fsr, self.mode, 0)
+            saved = _saved_plan(key)
+            h = ctypes.c_void_p()
+            _check(L.po2q_qconv2d_plan_create(ctypes.byref(h), -1 if saved is None else int(saved), *args,
+                                              self.bits, self.fsr, self.mode, 0))
+            self.plans.append(h)
+            self.ws.append(_workspace(L.po2q_qconv2d_plan_workspace_bytes(h), w.device))
+            self.w.append(w.contiguous())
+            self.xshape.append((N, C, H, W))
+            self.yshape.append((N, K, (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1))
+        n = len(self.plans)
+        self._n = n
+        self._pa = (ctypes.c_void_p * n)(*[h.value for h in self.plans])
+        self._wa = (ctypes.c_void_p * n)(*[w.data_ptr() for w in self.w])
+        self._sa = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self.ws])
+        self._ba = (ctypes.c_size_t * n)(*[t.numel() for t in self.ws])
+
+    def pack(self):
+        if self._n:
+            _check(self._L.po2q_qconv2d_plan_pack_batch(self._n, self._pa, self._wa, self._sa, self._ba,
+                                                        _stream(self.w[0].device)))
+
+    def conv(self, i, x):
+        _require_hip_f32(x, "input")
+        if tuple(x.shape) != self.xshape[i]:
+            raise Po2qError("po2q: PackedConvs layer %d was planned for input %s, got %s"
+                            % (i, self.xshape[i], tuple(x.shape)))
+        x = x.contiguous()
+        y = torch.empty(self.yshape[i], dtype=torch.float32, device=x.device)
+        ws = self.ws[i]
+        _check(self._L.po2q_qconv2d_plan_run_packed(self.plans[i], x.data_ptr(), self.w[i].data_ptr(), None,
+                                                    y.data_ptr(), None, None, None, 0, ws.data_ptr(), ws.numel(),
+                                                    _stream(x.device)))
+        return y
+
+    def __del__(self):
+        L = getattr(self, "_L", None)
+        for h in getattr(self, "plans", []):
+            if L is not None and h:
+                L.po2q_qconv2d_plan_destroy(h)
 
 
 def s2ds_supported(x_shape, bits=4, mode="po2", fsr=1):

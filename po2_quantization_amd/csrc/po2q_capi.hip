@@ -530,6 +530,70 @@ int po2q_qconv2d_plan_run(const po2q_conv_plan* plan, const float* x, const floa
                     reinterpret_cast<hipStream_t>(stream), e);
 }
 
+int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, const float* const* w,
+                                 void* const* workspace, const size_t* workspace_bytes, void* stream) {
+    using namespace po2q;
+    if (n < 0 || (n > 0 && (!plans || !w || !workspace || !workspace_bytes))) {
+        set_error("po2q: pack batch: null arrays");
+        return PO2Q_ERR_INVALID;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::vector<const ConvPlan*> bp;
+    std::vector<const float*> bw;
+    std::vector<uint16_t*> bpk;
+    std::vector<float*> bsc;
+    int bits = 0, fsr = 0, mode = 0;
+    for (int i = 0; i < n; ++i) {
+        const po2q_conv_plan* h = plans[i];
+        if (!h || !w[i] || !workspace[i]) {
+            set_error("po2q: pack batch: null plan, weight or workspace");
+            return PO2Q_ERR_INVALID;
+        }
+        const ConvPlan& p = h->p;
+        const WsLayout L = ws_layout(p, h->mode);
+        if (workspace_bytes[i] < L.total) {
+            set_error("po2q: pack batch: workspace too small (need " + std::to_string(L.total) + " bytes)");
+            return PO2Q_ERR_WORKSPACE;
+        }
+        const bool x3 = p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS;
+        if (x3 && p.fp) continue;  // the conv stages its own weight
+        const bool batchable = x3 && L.nparts == 0 && (bp.empty() || (h->bits == bits && h->fsr == fsr && h->mode == mode));
+        if (!batchable) {  // its own pack launch(es), as po2q_qconv2d_pack_f32
+            const int st = run_plan(p, nullptr, w[i], nullptr, nullptr, h->bits, h->fsr, h->mode, workspace[i],
+                                    workspace_bytes[i], s, ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_PACK);
+            if (st) return st;
+            continue;
+        }
+        bits = h->bits; fsr = h->fsr; mode = h->mode;
+        char* ws = reinterpret_cast<char*>(workspace[i]);
+        bp.push_back(&p);
+        bw.push_back(w[i]);
+        bpk.push_back(reinterpret_cast<uint16_t*>(ws + L.packed_off));
+        bsc.push_back(reinterpret_cast<float*>(ws + L.scale_off));
+    }
+    if (bp.empty()) return PO2Q_OK;
+    return hip_status(launch_pack_bf16x3_batch((int)bp.size(), bp.data(), bw.data(), bpk.data(), bsc.data(), bits, fsr,
+                                               mode, s),
+                      "batched weight pack launch");
+}
+
+int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias,
+                                 float* y, const float* post_scale, const float* post_shift, const float* residual,
+                                 int act, const void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace po2q;
+    if (!plan || !x || !w || !y || !workspace) {
+        set_error("po2q: null plan or pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (act < PO2Q_ACT_NONE || act > PO2Q_ACT_SILU) {
+        set_error("po2q: unknown activation " + std::to_string(act));
+        return PO2Q_ERR_INVALID;
+    }
+    const ConvEpi e{post_scale, post_shift, residual, act};
+    return run_plan(plan->p, x, w, bias, y, plan->bits, plan->fsr, plan->mode, const_cast<void*>(workspace),
+                    workspace_bytes, reinterpret_cast<hipStream_t>(stream), e, RUN_CONV);
+}
+
 int po2q_qconv2d_plan_describe(const po2q_conv_plan* plan, char* buf, size_t len) {
     if (!plan || !buf || len == 0) {
         po2q::set_error("po2q: null plan or buffer");

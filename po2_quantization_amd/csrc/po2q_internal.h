@@ -117,6 +117,11 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
                               int bits, int fsr, int mode, uint16_t* packed, float* scale_out,
                               hipStream_t s);
 
+// The same for n weight tensors (plans[i] bf16x3 kinds, fused absmax) in ceil(n / 16) launches.
+hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
+                                    uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
+                                    hipStream_t s);
+
 // Depthwise 3x3 LDS-halo kernel (po2q_conv_dw.hip): plan (kind KIND_DEPTHWISE, vrx 1) and launch
 // with the fused epilogue (ps / pb / res may be NULL, act PO2Q_ACT_*).
 bool dw3_plan(ConvPlan& p);

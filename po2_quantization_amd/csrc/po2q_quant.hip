@@ -173,11 +173,12 @@ struct PackX3 {
 // finishes in one or two rounds of independent loads per thread.
 constexpr int kPackThreads = 1024;
 
-__global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
-                                                               const unsigned* __restrict__ partial,
-                                                               int nparts, int lo, int hi, int mode,
-                                                               PackX3 pg, uint16_t* __restrict__ packed,
-                                                               float* __restrict__ scale_out) {
+// The pack of one weight tensor by block `bid` of `nb` (pack_bf16x3_kernel: one tensor per
+// launch; pack_bf16x3_batch_kernel: one tensor per blockIdx.y).
+__device__ __forceinline__ void pack_bf16x3_body(const float* __restrict__ w, int64_t n,
+                                                 const unsigned* __restrict__ partial, int nparts, int lo, int hi,
+                                                 int mode, const PackX3& pg, uint16_t* __restrict__ packed,
+                                                 float* __restrict__ scale_out, int bid, int nb) {
     __shared__ unsigned red[kPackThreads / 64];
     __shared__ unsigned thr[PO2Q_THR_COUNT];
     for (int i = threadIdx.x; i < PO2Q_THR_COUNT; i += kPackThreads) thr[i] = po2q_thr[mode > 0 ? 1 : 0][i];
@@ -212,14 +213,14 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
     m = block_max_u32<kPackThreads / 64>(m, red);
     const float scale = __uint_as_float(m);
     const bool fin = (m > 0u) && (m < 0x7f800000u);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = fin ? scale : 1.0f;
+    if (bid == 0 && threadIdx.x == 0) *scale_out = fin ? scale : 1.0f;
     // one 16-byte B fragment slot (8 consecutive k = 8 consecutive input channels of
     // one tap, one output channel) per thread and iteration; 32-bit index math
     const int OCT = pg.CC >> 3;
     const int RS = pg.R * pg.S;
     const int nfr = (int)(pg.total >> 3);
     uint4* out = reinterpret_cast<uint4*>(packed);
-    for (int j = blockIdx.x * kPackThreads + threadIdx.x; j < nfr; j += gridDim.x * kPackThreads) {
+    for (int j = bid * kPackThreads + threadIdx.x; j < nfr; j += nb * kPackThreads) {
         const int lane = j & 63;
         int t = j >> 6;
         int k, c0, tapoff;
@@ -276,18 +277,83 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
     }
 }
 
-hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned* partial, int nparts, int bits,
-                              int fsr, int mode, uint16_t* packed, float* scale_out, hipStream_t s) {
-    int lo, hi;
-    clamp_window(bits, fsr, lo, hi);
+__global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* __restrict__ w, int64_t n,
+                                                               const unsigned* __restrict__ partial,
+                                                               int nparts, int lo, int hi, int mode,
+                                                               PackX3 pg, uint16_t* __restrict__ packed,
+                                                               float* __restrict__ scale_out) {
+    pack_bf16x3_body(w, n, partial, nparts, lo, hi, mode, pg, packed, scale_out, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// Up to kPackBatch weight tensors quantized + packed in one launch (blockIdx.y = tensor):
+// the per-layer pack launches of a whole forward become ceil(n / kPackBatch) launches.
+struct PackJob {
+    const float* w;
+    uint16_t* packed;
+    float* scale;
+    int64_t n;
+    int lo, hi, mode, nb;
+    PackX3 pg;
+};
+constexpr int kPackBatch = 16;
+struct PackBatch {
+    PackJob job[kPackBatch];
+};
+
+__global__ __launch_bounds__(kPackThreads) void pack_bf16x3_batch_kernel(PackBatch B) {
+    const PackJob& j = B.job[blockIdx.y];
+    if ((int)blockIdx.x >= j.nb) return;  // block-uniform
+    pack_bf16x3_body(j.w, j.n, nullptr, 0, j.lo, j.hi, j.mode, j.pg, j.packed, j.scale, (int)blockIdx.x, j.nb);
+}
+
+static PackX3 pack_geom(const ConvPlan& p) {
     PackX3 pg;
     pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
     pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps;
     pg.vr = p.kind == KIND_BF16X3_ROWS ? 2 : (p.vrx ? 1 : 0);
     pg.total = p.packed_floats * 2;
+    return pg;
+}
+
+static int pack_blocks(const PackX3& pg) {
     int64_t b = (pg.total / 8 + kPackThreads - 1) / kPackThreads;  // one 16-byte fragment slot per thread
-    if (b < 1) b = 1;
-    if (b > 32) b = 32;
+    return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 32);
+}
+
+hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
+                                    uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
+                                    hipStream_t s) {
+    int lo, hi;
+    clamp_window(bits, fsr, lo, hi);
+    for (int i0 = 0; i0 < n; i0 += kPackBatch) {
+        PackBatch B;
+        const int m = std::min(kPackBatch, n - i0);
+        int nbmax = 1;
+        for (int i = 0; i < m; ++i) {
+            const ConvPlan& p = *plans[i0 + i];
+            PackJob& j = B.job[i];
+            j.w = w[i0 + i];
+            j.packed = packed[i0 + i];
+            j.scale = scale_out[i0 + i];
+            j.n = (int64_t)p.K * p.Cg * p.R * p.S;
+            j.lo = lo; j.hi = hi; j.mode = mode - 1;
+            j.pg = pack_geom(p);
+            j.nb = pack_blocks(j.pg);
+            nbmax = std::max(nbmax, j.nb);
+        }
+        hipLaunchKernelGGL(pack_bf16x3_batch_kernel, dim3((unsigned)nbmax, (unsigned)m), dim3(kPackThreads), 0, s, B);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned* partial, int nparts, int bits,
+                              int fsr, int mode, uint16_t* packed, float* scale_out, hipStream_t s) {
+    int lo, hi;
+    clamp_window(bits, fsr, lo, hi);
+    const PackX3 pg = pack_geom(p);
+    const int b = pack_blocks(pg);
     const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
     hipLaunchKernelGGL(pack_bf16x3_kernel, dim3((unsigned)b), dim3(kPackThreads), 0, s, w, n, partial, nparts, lo, hi,
                        mode - 1, pg, packed, scale_out);

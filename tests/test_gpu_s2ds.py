@@ -115,3 +115,24 @@ def test_basicblock_eval_fused_equals_module_sequence(stage, C, H, q, monkeypatc
         monkeypatch.setattr(qc, "INFERENCE_FUSION", False)
         ref = blk(x)
     assert nerr(y, ref) <= 1e-6, nerr(y, ref)
+
+
+def test_packed_convs_equal_per_layer_calls():
+    """_lib.PackedConvs (one batched weight-pack launch for every layer, then each conv from its
+    packed workspace) gives qconv2d()'s results bit for bit, layer by layer (ResNet56 stage-2 /
+    stage-3 shapes, a 1x1 stride-2 layer, and more layers than one 16-job launch holds)."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [((2, 32, 24, 24), (32, 32, 3, 3), 1, 1), ((2, 64, 12, 12), (64, 64, 3, 3), 1, 1),
+              ((2, 16, 24, 24), (32, 16, 1, 1), 2, 0)] * 6
+    specs, xs = [], []
+    for xs_, ws_, st, pad in shapes:
+        xs.append(torch.randn(xs_, generator=g).to(DEV))
+        specs.append((xs_, (torch.randn(ws_, generator=g) * 0.1).to(DEV), st, pad))
+    for q in ("po2", "po2+"):
+        ref = [_lib.qconv2d(x, w, None, st, pad, 1, 1, 4, q) for x, (_, w, st, pad) in zip(xs, specs)]
+        pc = _lib.PackedConvs(specs, 4, q)
+        pc.pack()
+        for i, x in enumerate(xs):
+            assert torch.equal(pc.conv(i, x), ref[i]), i
+        with pytest.raises(_lib.Po2qError, match="planned for input"):
+            pc.conv(0, xs[1])
