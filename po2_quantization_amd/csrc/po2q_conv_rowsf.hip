@@ -64,7 +64,8 @@ struct RowsFArgs {
 };
 
 // PD: raw ring slots (PD - 1 rows in flight ahead of the one being split).
-// NTS: non-temporal output stores.  EPI: fused eval-BN affine + activation.
+// NTS bit 0: non-temporal output stores, bit 1: non-temporal x loads.  EPI: fused eval-BN
+// affine + activation.
 // V (variant bits, autotune candidates): 1 = B fragments held in VGPRs for the kernel's
 // lifetime (no per-step LDS weight reads; C = 32: 72 VGPRs of weights, 2 waves per
 // SIMD, one block per CU), 2 = direct stores from the
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
         const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(2 * wave) * 1024u;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            rows_dma16<false>(rs, (hok && vi[i] != 0x7fffffffu && !(DBG & 4)) ? vi[i] + roff : 0x7fffffffu, 0u,
+            rows_dma16<(NTS & 2) != 0>(rs, (hok && vi[i] != 0x7fffffffu && !(DBG & 4)) ? vi[i] + roff : 0x7fffffffu, 0u,
                               base + i * 1024u);
         if constexpr (RES) {
             const int o = jn - 2;  // output row index within the segment
@@ -435,7 +436,7 @@ void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
     p.packed_floats = (int64_t)3 * p.steps * p.NT * 64 * 4;
     p.tilesQ = 1;
     // variants (plan field PS = V): C = 16: 0 plain, 1 VGPR weights, 2 direct stores;
-    // C = 32: 0 only.  nts: non-temporal stores (slower with 64-byte runs: C = 16 only)
+    // C = 32: 0 only.  nts: see the candidate loop
     const std::vector<int> vs = b.C == 16 ? std::vector<int>{0, 1, 2} : std::vector<int>{0, 1};
     for (int pd : {3, 4, 2}) {
         if (b.C == 16 && pd == 2) continue;
@@ -456,8 +457,11 @@ void rowsf_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 rbs.push_back({(double)((items + slots - 1) / slots) * (rb + 2), rb});
             }
             std::sort(rbs.begin(), rbs.end());
-            for (int nts : {0, 1}) {
-                if (nts && (b.C == 32 || v == 2)) continue;
+            // nts: bit 0 non-temporal stores (C = 16 only: slower with 64-byte runs), bit 1
+            // non-temporal x loads (the pair kernel's best mode, r02_pair_nt.log)
+            for (int nts : {0, 1, 2, 3}) {
+                if (nts && v == 2) continue;
+                if (b.C == 32 ? (nts & 1) != 0 : nts == 2) continue;
                 for (int i = 0; i < (int)rbs.size() && i < 2; ++i) {
                     ConvPlan c = q;
                     c.TP = rbs[i].second;
@@ -533,12 +537,17 @@ hipError_t launch_conv_rowsf(const ConvPlan& p, const float* x, const uint16_t* 
     if (p.C == c && p.pd == d && epi == e && p.nts == nt && p.PS == v) \
         return launch_rowsf_t<c, d, e, nt, v>(p, a, x, packed, scale, bias, y, s);
 #define PO2Q_RF16(d, e) \
-    PO2Q_RF(16, d, e, 0, 0) PO2Q_RF(16, d, e, 1, 0) PO2Q_RF(16, d, e, 0, 1) PO2Q_RF(16, d, e, 1, 1) PO2Q_RF(16, d, e, 0, 2)
+    PO2Q_RF(16, d, e, 0, 0) PO2Q_RF(16, d, e, 1, 0) PO2Q_RF(16, d, e, 0, 1) PO2Q_RF(16, d, e, 1, 1) PO2Q_RF(16, d, e, 0, 2) \
+    PO2Q_RF(16, d, e, 3, 0) PO2Q_RF(16, d, e, 3, 1)
     PO2Q_RF16(3, false) PO2Q_RF16(4, false) PO2Q_RF16(3, true) PO2Q_RF16(4, true)
     PO2Q_RF(32, 2, false, 0, 0) PO2Q_RF(32, 3, false, 0, 0) PO2Q_RF(32, 4, false, 0, 0)
     PO2Q_RF(32, 2, true, 0, 0) PO2Q_RF(32, 3, true, 0, 0) PO2Q_RF(32, 4, true, 0, 0)
     PO2Q_RF(32, 2, false, 0, 1) PO2Q_RF(32, 3, false, 0, 1) PO2Q_RF(32, 4, false, 0, 1)
     PO2Q_RF(32, 2, true, 0, 1) PO2Q_RF(32, 3, true, 0, 1) PO2Q_RF(32, 4, true, 0, 1)
+    PO2Q_RF(32, 2, false, 2, 0) PO2Q_RF(32, 3, false, 2, 0) PO2Q_RF(32, 4, false, 2, 0)
+    PO2Q_RF(32, 2, true, 2, 0) PO2Q_RF(32, 3, true, 2, 0) PO2Q_RF(32, 4, true, 2, 0)
+    PO2Q_RF(32, 2, false, 2, 1) PO2Q_RF(32, 3, false, 2, 1) PO2Q_RF(32, 4, false, 2, 1)
+    PO2Q_RF(32, 2, true, 2, 1) PO2Q_RF(32, 3, true, 2, 1) PO2Q_RF(32, 4, true, 2, 1)
 #undef PO2Q_RF16
 #undef PO2Q_RF
     return hipErrorInvalidValue;
@@ -559,6 +568,9 @@ hipError_t launch_conv_rowsf_res(const ConvPlan& p, const float* x, const uint16
     PO2Q_RFR(16, 4, 0, 0) PO2Q_RFR(16, 4, 1, 0) PO2Q_RFR(16, 4, 0, 1) PO2Q_RFR(16, 4, 1, 1) PO2Q_RFR(16, 4, 0, 2)
     PO2Q_RFR(32, 2, 0, 0) PO2Q_RFR(32, 3, 0, 0) PO2Q_RFR(32, 4, 0, 0)
     PO2Q_RFR(32, 2, 0, 1) PO2Q_RFR(32, 3, 0, 1) PO2Q_RFR(32, 4, 0, 1)
+    PO2Q_RFR(16, 3, 3, 0) PO2Q_RFR(16, 3, 3, 1) PO2Q_RFR(16, 4, 3, 0) PO2Q_RFR(16, 4, 3, 1)
+    PO2Q_RFR(32, 2, 2, 0) PO2Q_RFR(32, 3, 2, 0) PO2Q_RFR(32, 4, 2, 0)
+    PO2Q_RFR(32, 2, 2, 1) PO2Q_RFR(32, 3, 2, 1) PO2Q_RFR(32, 4, 2, 1)
 #undef PO2Q_RFR
     return hipErrorInvalidValue;
 }
