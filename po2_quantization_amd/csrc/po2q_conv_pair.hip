@@ -58,6 +58,7 @@ struct PairArgs {
     const float* pb2;
     int act1, act2;
     const float* res;  // RES: residual [N, C, H, W] added before act2
+    int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
 };
 
 // Channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P in a shared intermediate
@@ -440,6 +441,8 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
         // step 0's barrier publishes the zeros (and wl2)
     }
+    // static priority for the younger wave of each SIMD (MI355X_MICROARCH two-waves item 4)
+    if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
         step(std::integral_constant<int, 1>{}, j + 1);
@@ -521,16 +524,21 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 // ------------------------------------------------------------------ C ABI --
 namespace {
 
-// variant knob: PO2Q_PAIR_VARIANT = pd * 10 + nts (pd 2 / 3 x ring slots, nts bit 0:
-// non-temporal stores, bit 1 (pd 2 only): non-temporal x loads); default 23: non-temporal
+// variant knob: PO2Q_PAIR_VARIANT = prio * 100 + pd * 10 + nts (prio 1: waves 4.. at issue
+// priority 1; pd 2 / 3 x ring slots; nts bit 0: non-temporal stores, bit 1 (pd 2 only):
+// non-temporal x loads); default 23: non-temporal
 // loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32 (bs = 256,
 // profiles/r02_pair_nt.log)
-void pair_variant(int& pd, int& nts) {
+void pair_variant(int& pd, int& nts, int& prio, int64_t C) {
     pd = 2;
     nts = 3;
+    // priority 1 for waves 4..: 0.494 vs 0.504 / 0.500 ms at C = 16 (both store modes), mixed at
+    // C = 32 (profiles/r02_pair_prio.log)
+    prio = C == 16 ? 1 : 0;
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
         const int v = atoi(e);
-        const int d = v / 10, t = v % 10;
+        const int d = (v / 10) % 10, t = v % 10;
+        prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
         if ((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) {
             pd = d;
             nts = t;
@@ -582,8 +590,8 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // the pair is not the faster path, so the advisory says no (the kernel stays callable)
     if (C == 32 && !getenv("PO2Q_PAIR_C32")) return 0;  // PO2Q_PAIR_C32=1: advise it anyway (A/B runs)
     po2q::PairPlan pp;
-    int pd, nts;
-    pair_variant(pd, nts);
+    int pd, nts, prio;
+    pair_variant(pd, nts, prio, C);
     return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) &&
                    po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, true, pd, nts)
                ? 1
@@ -604,8 +612,8 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         return PO2Q_ERR_INVALID;
     }
     po2q::PairPlan pp;
-    int pd, nts;
-    pair_variant(pd, nts);
+    int pd, nts, prio;
+    pair_variant(pd, nts, prio, C);
     if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, residual != nullptr, pd, nts)) {
         po2q::set_error("po2q: pair: no plan for this shape");
         return PO2Q_ERR_UNSUPPORTED;
@@ -624,6 +632,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.ps1 = post_scale1; a.pb1 = post_shift1; a.act1 = act1;
     a.ps2 = post_scale2; a.pb2 = post_shift2; a.act2 = act2;
     a.res = residual;
+    a.prio = prio;
     const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {
         po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));
