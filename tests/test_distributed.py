@@ -55,5 +55,49 @@ def test_sharded_gather_and_max_over_ranks_timing(tmp_path):
     assert res[0]["dt"] >= 3 * 0.1                             # covers the slower rank's 3 timed steps
 
 
+def _cpu_standins(setattr_=setattr):
+    """Test-only: the chain's native calls replaced by the oracle's CPU restatement (the GPU
+    kernels have no CPU path), so the sharding itself runs here."""
+    from oracle import oracle as O
+    from po2_quantization_amd import _lib
+
+    setattr_(_lib, "qconv2d", lambda x, w, b, st, pad, d, g, bits, mode, fsr=1, precision="auto":
+             O.cpu_reference_qconv2d(x, w, b, st, pad, d, g, bits, mode))
+    setattr_(_lib, "pair_supported", lambda *a, **k: False)
+    setattr_(_lib, "s2ds_supported", lambda *a, **k: False)
+
+
+def _chain_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    _cpu_standins()
+    chain = bench.QConvChain(3, 10, "po2", 4, "auto", torch.device("cpu"), seed=0)  # replicated weights
+    x = torch.relu(torch.randn(2, 16, 8, 8, generator=torch.Generator().manual_seed(100 + rank)))
+    gathered = torch.empty(world * 2, 10)
+    with torch.no_grad():
+        out = bench.gather_logits(chain.forward(x), gathered, world)
+    torch.save({"gathered": out.clone(), "x": x}, os.path.join(out_dir, "c%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+def test_sharded_qconv_chain_equals_full_batch(tmp_path, monkeypatch):
+    """bench.py's data-parallel step: each rank runs the ResNet20 quantized-conv chain (56-layer
+    chain's structure at n = 3 blocks) on its own batch shard with the same seeded weights, and
+    the all_gather of the logits equals the chain run on the whole batch in one process."""
+    world = 2
+    mp.spawn(_chain_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / ("c%d.pt" % r), weights_only=True) for r in range(world)]
+    import bench
+
+    _cpu_standins(monkeypatch.setattr)
+    chain = bench.QConvChain(3, 10, "po2", 4, "auto", torch.device("cpu"), seed=0)
+    with torch.no_grad():
+        full = chain.forward(torch.cat([res[r]["x"] for r in range(world)]))
+    for r in range(world):
+        assert torch.allclose(res[r]["gathered"], full, rtol=1e-5, atol=1e-6)
+
+
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
