@@ -59,6 +59,7 @@ struct PairArgs {
     int act1, act2;
     const float* res;  // RES: residual [N, C, H, W] added before act2
     int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
+    int halves;        // C = 16, 1: store 64-byte half lines as the MFMA layout holds them (A/B knob)
 };
 
 // Channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P in a shared intermediate
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
             const bool orow = o >= 0 && o < rbe;
             const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
             const int g = lane >> 4;
+            floatx4 vv[NT][NG];
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 const int ch = 16 * nt + (lane & 15);
@@ -312,10 +314,39 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
                     }
-                    const int q = q0 + ql;
-                    rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    vv[nt][grp] = v;
+                    if (CC != 16 || a.halves) {
+                        const int q = q0 + ql;
+                        rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                    }
                     acc2[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
                 }
+            }
+            if (CC == 16 && !a.halves) {
+                // Whole 128-byte lines per store: lane L holds pixels 4g .. 4g + 3 (vv[0][0]) and
+                // 16 + 4g .. (vv[0][1]) of channel L & 15.  One row_ror:8 DPP exchange within each
+                // 16-lane row gives store A channels 0-7 (lanes with bit 3 set take channel L & 7's
+                // second half from lane L - 8) and store B channels 8-15 (lanes without it take
+                // channel 8 + (L & 7)'s first half from lane L + 8): 8 lanes x 16 bytes = one full
+                // line per channel, where two 64-byte halves from two stores cost partial-line
+                // writes (PMC: 1.32x the output bytes with non-temporal stores).
+                const bool hi8 = (lane & 8) != 0;
+                floatx4 sa, sb;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float r1 = __int_as_float(
+                        __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][NG - 1][e]), 0x128, 0xf, 0xf, false));
+                    const float r0 = __int_as_float(
+                        __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][0][e]), 0x128, 0xf, 0xf, false));
+                    sa[e] = hi8 ? r1 : vv[0][0][e];
+                    sb[e] = hi8 ? vv[0][NG - 1][e] : r0;
+                }
+                const int q = q0 + (hi8 ? 16 : 0) + 4 * g;
+                const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
+                const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
+                const bool ok = orow && q < a.W;
+                rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+                rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
             }
         }
 
@@ -524,19 +555,23 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 // ------------------------------------------------------------------ C ABI --
 namespace {
 
-// variant knob: PO2Q_PAIR_VARIANT = prio * 100 + pd * 10 + nts (prio 1: waves 4.. at issue
+// variant knob: PO2Q_PAIR_VARIANT = halves * 1000 + prio * 100 + pd * 10 + nts (halves 1: C = 16
+// stores 64-byte half lines; prio 1: waves 4.. at issue
 // priority 1; pd 2 / 3 x ring slots; nts bit 0: non-temporal stores, bit 1 (pd 2 only):
 // non-temporal x loads); default 23: non-temporal
 // loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32 (bs = 256,
 // profiles/r02_pair_nt.log)
-void pair_variant(int& pd, int& nts, int& prio, int64_t C) {
+void pair_variant(int& pd, int& nts, int& prio, int& halves, int64_t C) {
     pd = 2;
     nts = 3;
     // priority 1 for waves 4..: 0.494 vs 0.504 / 0.500 ms at C = 16 (both store modes), mixed at
     // C = 32 (profiles/r02_pair_prio.log)
     prio = C == 16 ? 1 : 0;
+    halves = 0;
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
-        const int v = atoi(e);
+        int v = atoi(e);
+        halves = v >= 1000 ? 1 : 0;  // + 1000: 64-byte half-line stores (C = 16)
+        v %= 1000;
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
         if ((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) {
@@ -590,8 +625,8 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // the pair is not the faster path, so the advisory says no (the kernel stays callable)
     if (C == 32 && !getenv("PO2Q_PAIR_C32")) return 0;  // PO2Q_PAIR_C32=1: advise it anyway (A/B runs)
     po2q::PairPlan pp;
-    int pd, nts, prio;
-    pair_variant(pd, nts, prio, C);
+    int pd, nts, prio, halves;
+    pair_variant(pd, nts, prio, halves, C);
     return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) &&
                    po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, true, pd, nts)
                ? 1
@@ -612,8 +647,8 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         return PO2Q_ERR_INVALID;
     }
     po2q::PairPlan pp;
-    int pd, nts, prio;
-    pair_variant(pd, nts, prio, C);
+    int pd, nts, prio, halves;
+    pair_variant(pd, nts, prio, halves, C);
     if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, residual != nullptr, pd, nts)) {
         po2q::set_error("po2q: pair: no plan for this shape");
         return PO2Q_ERR_UNSUPPORTED;
@@ -633,6 +668,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.ps2 = post_scale2; a.pb2 = post_shift2; a.act2 = act2;
     a.res = residual;
     a.prio = prio;
+    a.halves = halves;
     const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {
         po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));

@@ -53,7 +53,7 @@ SHAPES = [(2, 20, 32, 16), (1, 9, 224, 16), (3, 37, 68, 16), (2, 1, 36, 16), (1,
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
-@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123"])
+@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123", "1123"])
 def test_pair_chain_vs_torch(shape, variant, monkeypatch):
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", variant)
     N, H, W, C = shape
