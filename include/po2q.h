@@ -263,7 +263,8 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
  * x [N, C, H, W], w [2C, C, 3, 3], wds [2C, C, 1, 1] (each quantized with its own max|w|,
  * the same bits / fsr / mode), y and yds [N, 2C, P, Q]; x is read once for both.  Every
  * epilogue pointer may be NULL.  C = 16 or 32, W % 4 == 0, po2 / po2+; no workspace.
- * po2q_qconv2d_s2ds_supported: 1 when the shape takes it.
+ * po2q_qconv2d_s2ds_supported: 1 when the shape takes it AND it is the faster path (W >= 96;
+ * on CIFAR-size rows two launches are faster).
  */
 int po2q_qconv2d_s2ds_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
 int po2q_qconv2d_s2ds_f32(const float* x, const float* w, const float* wds, float* y, float* yds,

@@ -524,8 +524,9 @@ class PackedConvs:
 
 
 def s2ds_supported(x_shape, bits=4, mode="po2", fsr=1):
-    """True when qconv2d_s2ds takes this input shape (C = 16 or 32 -> 2C, W % 4 == 0, po2 / po2+)."""
-    if mode not in ("po2", "po2+"):
+    """True when qconv2d_s2ds takes this input shape (C = 16 or 32 -> 2C, W % 4 == 0, po2 / po2+).
+    PO2Q_S2DS=0 turns the fused transition off (A/B runs)."""
+    if mode not in ("po2", "po2+") or os.environ.get("PO2Q_S2DS") == "0":
         return False
     N, C, H, W = (int(v) for v in x_shape)
     return bool(load().po2q_qconv2d_s2ds_supported(N, C, H, W, int(bits), int(fsr), MODES[mode]))

@@ -503,6 +503,10 @@ bool s2ds_plan(po2q::ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, in
 }  // namespace
 
 int po2q_qconv2d_s2ds_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode) {
+    // advisory: the fused transition is the faster path on wide rows (ResNet56 @224: W = 224 /
+    // 112), slower on CIFAR-size rows (@32, W = 32 / 16: 2.17-2.20 vs 2.02-2.08 ms per forward,
+    // profiles/r02_ab_s2ds_small.txt); po2q_qconv2d_s2ds_f32 itself takes both
+    if (W < 96) return 0;
     po2q::ConvPlan p;
     return s2ds_plan(p, N, C, H, W, bits, fsr, mode) ? 1 : 0;
 }
