@@ -200,20 +200,6 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
                           int bits, int fsr, int mode, int flags, char* buf, size_t len);
 
 /*
- * Plan handles: a conv problem resolved ONCE to its kernel plan (the tuned plan when
- * po2q_qconv2d_autotune has measured it in this process, else the heuristic one; or
- * candidate `index` >= 0 of po2q_qconv2d_plans), so a framework binding that caches the
- * handle per problem pays no planning cost per call.  The PyTorch extension
- * (po2_quantization_amd/csrc/po2q_torch.cpp: torch.ops.po2q.*) keeps one per shape key.
- *   po2q_qconv2d_plan_create            resolve (same arguments as po2q_qconv2d_f32 + index)
- *   po2q_qconv2d_plan_workspace_bytes   the workspace THIS plan needs
- *   po2q_qconv2d_plan_run               quantize + conv (+ the fused epilogue of
- *                                       po2q_qconv2d_fused_f32: post_scale / post_shift /
- *                                       residual may be NULL, act PO2Q_ACT_*) on `stream`
- * Handles are immutable after creation; run may be called concurrently on one handle.
- * Replaces per call: QuantizedConv2d.forward (models/quantized_conv.py:32-38).
- */
-/*
  * QAT backward, weight gradient: the gradient autograd takes through
  * F.conv2d(x, Q(w), ...) for w -- the straight-through estimator passes it unchanged
  * (utils/quantizers.py:34-36; train.py:79-91 runs loss.backward()):
@@ -236,14 +222,15 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw,
 /*
  * Two chained quantized convs in one launch (ResNet56 stage-1 BasicBlock, reference
  * models/resnet.py:55-71; each conv is QuantizedConv2d.forward, models/quantized_conv.py:
- * 32-38): 3x3 / stride 1 / pad 1, 16 -> 16 -> 16 channels, x [N,16,H,W], w1 / w2 [16,16,3,3]
- * quantized with the same (bits, fsr, mode):
+ * 32-38; stage 2 takes it too): 3x3 / stride 1 / pad 1, C -> C -> C channels with C = 16 or
+ * 32, x [N,C,H,W], w1 / w2 [C,C,3,3] quantized with the same (bits, fsr, mode):
  *   y = act2(conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 (+ residual))
  *   h = act1((conv(x, Q(w1)) + bias1) * post_scale1 + post_shift1)
  * (every pointer but x, w1, w2, y may be NULL).  h never leaves the chip.  No workspace.
- * po2q_qconv2d_pair_f32 takes W % 4 == 0, W <= 224, C == 16, mode po2 / po2+ with the
- * exponent window inside bf16's range.  po2q_qconv2d_pair_supported: 1 when it takes the
- * shape AND is the faster path (C = 16, W >= 128; otherwise two single-conv calls).
+ * po2q_qconv2d_pair_f32 takes C in {16, 32}, W % 4 == 0, W <= 7 * 512 / C (224 for C = 16,
+ * 112 for C = 32), mode po2 / po2+ with the exponent window inside bf16's range.
+ * po2q_qconv2d_pair_supported: 1 when it takes the shape AND is the faster path (C = 16 with
+ * W >= 128; C = 32 only when PO2Q_PAIR_C32 is set; otherwise two single-conv calls).
  */
 int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
 int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, float* y,
@@ -272,6 +259,20 @@ int po2q_qconv2d_s2ds_f32(const float* x, const float* w, const float* wds, floa
                           const float* post_scale, const float* post_shift, int act,
                           const float* post_scale_ds, const float* post_shift_ds, void* stream);
 
+/*
+ * Plan handles: a conv problem resolved ONCE to its kernel plan (the tuned plan when
+ * po2q_qconv2d_autotune has measured it in this process, else the heuristic one; or
+ * candidate `index` >= 0 of po2q_qconv2d_plans), so a framework binding that caches the
+ * handle per problem pays no planning cost per call.  The PyTorch extension
+ * (po2_quantization_amd/csrc/po2q_torch.cpp: torch.ops.po2q.*) keeps one per shape key.
+ *   po2q_qconv2d_plan_create            resolve (same arguments as po2q_qconv2d_f32 + index)
+ *   po2q_qconv2d_plan_workspace_bytes   the workspace THIS plan needs
+ *   po2q_qconv2d_plan_run               quantize + conv (+ the fused epilogue of
+ *                                       po2q_qconv2d_fused_f32: post_scale / post_shift /
+ *                                       residual may be NULL, act PO2Q_ACT_*) on `stream`
+ * Handles are immutable after creation; run may be called concurrently on one handle.
+ * Replaces per call: QuantizedConv2d.forward (models/quantized_conv.py:32-38).
+ */
 typedef struct po2q_conv_plan po2q_conv_plan;
 int po2q_qconv2d_plan_create(po2q_conv_plan** out, int index,
                              int64_t N, int64_t C, int64_t H, int64_t W,

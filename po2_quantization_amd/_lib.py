@@ -467,7 +467,12 @@ class PackedConvs:
 
     specs: [(x_shape, w, stride, padding)] in call order (groups 1, dilation 1, no bias); the
     plans are resolved once here, so create it after the shapes were autotuned.  Call pack()
-    once per forward (after any weight update), then conv(i, x) for each layer."""
+    once per forward (after any weight update), then conv(i, x) for each layer.
+
+    The weights are held by reference and read at every pack(): they must be contiguous and
+    updated in place (an optimizer step, copy_); a module whose .weight is replaced by another
+    tensor (.to(), reassignment) needs a new PackedConvs.  pack() checks that every held
+    tensor still has the storage it had here."""
 
     def __init__(self, specs, bits=4, mode="po2", fsr=1):
         L = load()
@@ -476,6 +481,8 @@ class PackedConvs:
         self.plans, self.ws, self.w, self.xshape, self.yshape = [], [], [], [], []
         for x_shape, w, stride, padding in specs:
             _require_hip_f32(w, "weight")
+            if not w.is_contiguous():
+                raise Po2qError("po2q: PackedConvs needs contiguous weights (it reads them in place at every pack)")
             N, C, H, W = (int(v) for v in x_shape)
             K, _, R, S = w.shape
             sh, sw = _pair(stride)
@@ -488,17 +495,22 @@ class PackedConvs:
                                               self.bits, self.fsr, self.mode, 0))
             self.plans.append(h)
             self.ws.append(_workspace(L.po2q_qconv2d_plan_workspace_bytes(h), w.device))
-            self.w.append(w.contiguous())
+            self.w.append(w)
             self.xshape.append((N, C, H, W))
             self.yshape.append((N, K, (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1))
         n = len(self.plans)
         self._n = n
         self._pa = (ctypes.c_void_p * n)(*[h.value for h in self.plans])
-        self._wa = (ctypes.c_void_p * n)(*[w.data_ptr() for w in self.w])
+        self._wptr = [w.data_ptr() for w in self.w]
+        self._wa = (ctypes.c_void_p * n)(*self._wptr)
         self._sa = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self.ws])
         self._ba = (ctypes.c_size_t * n)(*[t.numel() for t in self.ws])
 
     def pack(self):
+        for i, w in enumerate(self.w):
+            if w.data_ptr() != self._wptr[i]:
+                raise Po2qError("po2q: PackedConvs weight %d changed storage since construction "
+                                "(set_() / resize); build a new PackedConvs" % i)
         if self._n:
             _check(self._L.po2q_qconv2d_plan_pack_batch(self._n, self._pa, self._wa, self._sa, self._ba,
                                                         _stream(self.w[0].device)))

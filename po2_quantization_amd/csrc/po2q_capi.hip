@@ -416,8 +416,27 @@ static int pick_split_plan(ConvPlan& p, int index, int64_t N, int64_t C, int64_t
                            int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                            int64_t groups, int mode, int bits, int fsr, int flags) {
     const int st = pick_plan(p, index, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags);
+    if (st) return st;
+    if (p.kind == KIND_BF16X3_ROWS && p.vrx == 5) {
+        // the stride-2 full-row kernel only exists with fused staging (it has no pre-packed
+        // twin): take the first candidate that reads a packed weight instead
+        std::vector<ConvPlan> cands;
+        if (!plan_candidates(cands, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags))
+            return PO2Q_ERR_INVALID;
+        bool found = false;
+        for (const ConvPlan& c : cands)
+            if (!c.fp && !(c.kind == KIND_BF16X3_ROWS && c.vrx == 5)) {
+                p = c;
+                found = true;
+                break;
+            }
+        if (!found) {
+            set_error("po2q: no pre-packed plan for this shape (split enqueue)");
+            return PO2Q_ERR_UNSUPPORTED;
+        }
+    }
     p.fp = 0;
-    return st;
+    return PO2Q_OK;
 }
 
 int po2q_qconv2d_pack_f32(int plan, const float* w, int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,

@@ -10,7 +10,7 @@
 //                        (models/quantized_conv.py:32-38)
 //   po2q::qconv2d_fused  the same + eval BatchNorm affine, residual add and activation of
 //                        the blocks (resnet.py:55-71, mobilenet.py:32-33, mobile_vit.py:20-21)
-//   po2q::qconv2d_pair   two chained 16-channel 3x3 qconvs (+ BN / act between and after, residual)
+//   po2q::qconv2d_pair   two chained C -> C 3x3 qconvs (C = 16 or 32) (+ BN / act between and after, residual)
 //   po2q::qconv2d_s2ds   a stage's 3x3 stride-2 conv1 + 1x1 stride-2 shortcut on one read of x
 //                        in one launch: a ResNet56 stage-1 BasicBlock (resnet.py:55-71)
 //   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
@@ -244,6 +244,17 @@ at::Tensor conv_wgrad(const at::Tensor& x_, const at::Tensor& dy_, at::IntArrayR
     const int64_t sh = pick(stride, 0, "stride"), sw = pick(stride, 1, "stride");
     const int64_t ph = pick(padding, 0, "padding"), pw = pick(padding, 1, "padding");
     const int64_t dh = pick(dilation, 0, "dilation"), dw = pick(dilation, 1, "dilation");
+    // the C ABI takes no dy / gw shapes: they must be the geometry's, or the kernel would read
+    // past dy or write past gw
+    TORCH_CHECK(groups >= 1 && wshape[0] > 0 && wshape[0] % groups == 0 && wshape[1] * groups == x.size(1),
+                "po2q: wgrad: weight shape ", wshape, " with groups=", groups, " does not match input channels ",
+                x.size(1));
+    TORCH_CHECK(sh > 0 && sw > 0 && dh > 0 && dw > 0 && ph >= 0 && pw >= 0, "po2q: wgrad: bad stride / padding / dilation");
+    const int64_t P = (x.size(2) + 2 * ph - dh * (wshape[2] - 1) - 1) / sh + 1;
+    const int64_t Q = (x.size(3) + 2 * pw - dw * (wshape[3] - 1) - 1) / sw + 1;
+    TORCH_CHECK(dy.size(0) == x.size(0) && dy.size(1) == wshape[0] && dy.size(2) == P && dy.size(3) == Q,
+                "po2q: wgrad: grad_output shape ", dy.sizes(), " is not [", x.size(0), ", ", wshape[0], ", ", P, ", ",
+                Q, "]");
     const size_t wsb = po2q_qconv2d_wgrad_workspace_bytes(x.size(0), x.size(1), x.size(2), x.size(3), wshape[0],
                                                           wshape[2], wshape[3], sh, sw, ph, pw, dh, dw, groups);
     TORCH_CHECK(wsb > 0, last_error());

@@ -70,9 +70,11 @@ class BasicBlock(nn.Module):
         the same native PO2 quantizer and bits, bf16x3 arithmetic allowed."""
         c1, c2 = self.conv1, self.conv2
         mode = NATIVE_MODES.get(c1.quantize_fn)
-        return (self.downsample is None and mode in ("po2", "po2+") and c2.quantize_fn is c1.quantize_fn
+        geom = all(tuple(c.kernel_size) == (3, 3) and tuple(c.stride) == (1, 1) and tuple(c.padding) == (1, 1)
+                   and tuple(c.dilation) == (1, 1) and c.groups == 1 and c.padding_mode == "zeros" for c in (c1, c2))
+        return (self.downsample is None and geom and mode in ("po2", "po2+") and c2.quantize_fn is c1.quantize_fn
                 and c1.bits == c2.bits and c1.in_channels in (16, 32) and c1.out_channels == c1.in_channels
-                and c2.out_channels == c1.in_channels and tuple(c1.stride) == (1, 1) and c1.precision != "fp32"
+                and c2.in_channels == c1.in_channels and c2.out_channels == c1.in_channels and c1.precision != "fp32"
                 and c2.precision != "fp32" and c1.bias is None and c2.bias is None
                 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
                 and _lib.pair_supported(x.shape, c1.bits, mode))
@@ -82,13 +84,16 @@ class BasicBlock(nn.Module):
         BatchNorm, models/resnet.py:100-105) eligible for the fused stride-2 kernel: same native PO2
         quantizer and bits, bf16x3 arithmetic allowed, no biases."""
         c1, ds = self.conv1, self.downsample
-        if ds is None or len(ds) != 2 or not isinstance(ds[0], QuantizedConv2d):
+        if (ds is None or len(ds) != 2 or not isinstance(ds[0], QuantizedConv2d)
+                or not isinstance(ds[1], nn.modules.batchnorm._BatchNorm)):
             return False
         d = ds[0]
         mode = NATIVE_MODES.get(c1.quantize_fn)
         return (mode in ("po2", "po2+") and d.quantize_fn is c1.quantize_fn and d.bits == c1.bits
                 and c1.in_channels in (16, 32) and c1.out_channels == 2 * c1.in_channels
-                and tuple(c1.stride) == (2, 2) and tuple(c1.padding) == (1, 1) and tuple(c1.dilation) == (1, 1)
+                and tuple(c1.kernel_size) == (3, 3) and tuple(c1.stride) == (2, 2) and tuple(c1.padding) == (1, 1)
+                and tuple(c1.dilation) == (1, 1) and c1.padding_mode == "zeros" and d.padding_mode == "zeros"
+                and tuple(d.dilation) == (1, 1)
                 and d.in_channels == c1.in_channels and d.out_channels == c1.out_channels
                 and tuple(d.kernel_size) == (1, 1) and tuple(d.stride) == (2, 2) and tuple(d.padding) == (0, 0)
                 and c1.groups == 1 and d.groups == 1 and c1.bias is None and d.bias is None

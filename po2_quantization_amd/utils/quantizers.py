@@ -7,8 +7,11 @@ Same names, call forms and error behaviour as the reference:
   quantize_model(model, quantizer, bits) -> float  utils/quantizers.py:139-153
   quantizer_dict {"lin", "lin+", "po2", "po2+"}    utils/quantizers.py:156-161
 
-PO2 / PO2+ run on the hand-written HIP kernels of libpo2q (fp32 HIP tensors
-only; anything else raises — there is no CPU path).  Backward is the
+PO2 / PO2+ on fp32 HIP tensors run on the hand-written HIP kernels of libpo2q.
+The reference's quantizers take any tensor (they are plain torch ops), so CPU,
+fp64 and bf16 inputs go to _lib.restated_quantize, the product-side torch
+restatement of the same threshold-table decision (bit-exact with the reference
+on tests/golden/quant_kat_dtypes.npz); the conv itself has no CPU path.  Backward is the
 straight-through estimator of the reference (:34-36, :54-56).
 
 LinearPowerOfTwo(Plus)Quantizer (utils/quantizers.py:59-136)

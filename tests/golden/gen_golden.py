@@ -234,11 +234,43 @@ def gen_models():
     print("models.npz:", sorted(out))
 
 
+WIDE_SPECS = [
+    # (model, image, batch, quantizer, bits, input seed): wide enough that the drop-in's eval
+    # forward takes the fused-block kernels -- the stage-1 conv pair (W >= 128) and the
+    # stride-2 + shortcut kernel (transition input W >= 96) -- on the reference's logits
+    ("resnet56", 128, 2, "po2", 4, 3),
+    ("resnet20", 224, 1, "po2+", 4, 4),
+]
+
+
+def gen_models_wide():
+    """models_wide.npz: QAT-mode eval logits of ResNet56 @128 and ResNet20 @224 (reference
+    models/resnet.py:55-71 BasicBlock, :150-163 projection shortcut, :190-201 forward)."""
+    from models.model import get_model
+    from utils.quantizers import quantizer_dict
+
+    out = {}
+    for mt, sz, bs, q, bits, seed in WIDE_SPECS:
+        m = get_model(mt, 10, quantizer_dict[q], bits, (sz, sz))
+        seeded_fill_(m, seed=7)
+        m.eval()
+        x = torch.randn(bs, 3, sz, sz, generator=torch.Generator().manual_seed(seed))
+        with torch.no_grad():
+            logits = m(x)
+        tag = "%s@%d/%s/%d" % (mt, sz, q, bits)
+        out["x/" + tag] = x.numpy()
+        out["logits/" + tag] = logits.numpy()
+    np.savez_compressed(os.path.join(HERE, "models_wide.npz"), **out)
+    print("models_wide.npz:", sorted(out))
+
+
 def main():
     sys.path.insert(0, REF)
     thr = json.load(open(os.path.join(HERE, "po2_thresholds.json")))["modes"]
     torch.set_num_threads(8)
-    parts = sys.argv[1:] or ["quant", "conv", "lin", "models"]  # e.g. `gen_golden.py lin`
+    parts = sys.argv[1:] or ["quant", "conv", "lin", "models", "wide"]  # e.g. `gen_golden.py lin`
+    if "wide" in parts:
+        gen_models_wide()
     if "quant" in parts:
         gen_quant(thr)
     if "conv" in parts:

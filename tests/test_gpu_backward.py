@@ -95,6 +95,20 @@ def test_wgrad_deterministic_and_unsupported():
         _lib.conv_wgrad(x, gy, (16, 32, 5, 5), 1, 2)
 
 
+def test_wgrad_rejects_mismatched_shapes():
+    """The C ABI takes no grad_output / gradient shapes, so the op checks them: a weight whose
+    input channels differ from x's, or a grad_output that is not [N, K, P, Q], raises instead of
+    reading or writing out of bounds."""
+    x = torch.randn(2, 32, 12, 12, device=DEV)
+    gy = torch.randn(2, 16, 12, 12, device=DEV)
+    with pytest.raises(RuntimeError, match="does not match input channels"):
+        _lib.conv_wgrad(x, gy, (16, 16, 3, 3), 1, 1)
+    with pytest.raises(RuntimeError, match="grad_output shape"):
+        _lib.conv_wgrad(x, torch.randn(2, 16, 11, 12, device=DEV), (16, 32, 3, 3), 1, 1)
+    with pytest.raises(RuntimeError, match="grad_output shape"):
+        _lib.conv_wgrad(x, torch.randn(2, 8, 12, 12, device=DEV), (16, 32, 3, 3), 1, 1)
+
+
 WGRAD_SHAPES = [  # N, C, H, W, K, R, stride, pad, dilation
     (2, 3, 32, 32, 16, 3, 1, 1, 1),     # stem: C = 3
     (3, 16, 33, 30, 16, 3, 1, 1, 1),    # ragged rows, Q % 4 != 0 (scalar loads)

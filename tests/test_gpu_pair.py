@@ -117,3 +117,59 @@ def test_pair_rejects():
         _lib.qconv2d_pair(x, w, w)
     with pytest.raises(_lib.Po2qError, match="mode"):
         _lib.qconv2d_pair(torch.randn(1, 16, 8, 8, device=DEV), w, w, mode="none")
+
+
+def oracle_block(x, w1, w2, mode, e, act1, act2, res, bias1=None):
+    """The reference BasicBlock chain (models/resnet.py:55-71) on the oracle: O.qconv2d (fp64
+    accumulation on the bit-exact Q(w)) -> numpy affine / activation -> O.qconv2d -> + residual ->
+    activation.  Test-only checker."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    acts = {"none": lambda t: t, "relu": lambda t: np.maximum(t, 0.0),
+            "relu6": lambda t: np.clip(t, 0.0, 6.0), "silu": lambda t: t / (1.0 + np.exp(-t))}
+    v = lambda k: e[k].cpu().numpy().astype(np.float64).reshape(1, -1, 1, 1)  # noqa: E731
+    h, _ = O.qconv2d(x.cpu().numpy(), w1.cpu().numpy(), None if bias1 is None else bias1.cpu().numpy(),
+                     1, 1, 1, 1, 4, mode)
+    if "post_scale1" in e:
+        h = h * v("post_scale1") + v("post_shift1")
+    h = acts[act1](h).astype(np.float32)  # the intermediate is an fp32 tensor in the reference
+    y, _ = O.qconv2d(h, w2.cpu().numpy(), None, 1, 1, 1, 1, 4, mode)
+    if "post_scale2" in e:
+        y = y * v("post_scale2") + v("post_shift2")
+    if res is not None:
+        y = y + res.cpu().numpy().astype(np.float64)
+    return acts[act2](y)
+
+
+ORACLE_SHAPES = [(1, 9, 224, 16), (2, 12, 128, 16), (1, 10, 68, 16), (2, 7, 112, 32), (1, 11, 64, 32)]
+
+
+@pytest.mark.parametrize("shape", ORACLE_SHAPES, ids=[str(s) for s in ORACLE_SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+"])
+def test_pair_vs_oracle(shape, mode):
+    """conv_pair against the oracle (C restatement of the reference quantizer + fp64 conv), the
+    plain chain: max|y - y_oracle| <= 1e-5 max|y_oracle|."""
+    from tests._util import normwise_err
+
+    N, H, W, C = shape
+    x, w1, w2, _ = make(N, H, W, 101 + H, False, C)
+    y = _lib.qconv2d_pair(x, w1, w2, 4, mode)
+    ref = oracle_block(x, w1, w2, mode, {}, "none", "none", None)
+    assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL, normwise_err(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("C,W", [(16, 224), (16, 96 + 32), (32, 112), (32, 64)])
+def test_pair_block_vs_oracle(C, W):
+    """The BasicBlock form BasicBlock.forward uses (E = 1 epilogues): BN affine + ReLU, conv 2,
+    BN affine, + identity shortcut, ReLU, against the oracle chain."""
+    from tests._util import normwise_err
+
+    x, w1, w2, e = make(2, 9, W, 7 + W, True, C)
+    g = torch.Generator().manual_seed(9)
+    b1 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    for mode in ("po2", "po2+"):
+        y = _lib.qconv2d_pair(x, w1, w2, 4, mode, bias1=b1, act1="relu", act2="relu", residual=x, **e)
+        ref = oracle_block(x, w1, w2, mode, e, "relu", "relu", x, bias1=b1)
+        assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL, (mode, normwise_err(y.cpu().numpy(), ref))

@@ -138,3 +138,47 @@ def test_packed_convs_equal_per_layer_calls():
             assert torch.equal(pc.conv(i, x), ref[i]), i
         with pytest.raises(_lib.Po2qError, match="planned for input"):
             pc.conv(0, xs[1])
+
+
+ORACLE_SHAPES = [(1, 16, 12, 224), (2, 16, 9, 128), (1, 32, 10, 112), (2, 32, 7, 96), (1, 16, 5, 40)]
+
+
+@pytest.mark.parametrize("shape", ORACLE_SHAPES, ids=[str(s) for s in ORACLE_SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+"])
+def test_s2ds_vs_oracle(shape, mode):
+    """Both outputs of the fused stride-2 transition against the oracle (C restatement of the
+    reference quantizer + fp64 conv): conv1 3x3 s2 p1 and downsample.0 1x1 s2 p0, each with its
+    own Q(w) (reference models/resnet.py:55-71, :150-163)."""
+    from oracle import oracle as O
+    from tests._util import normwise_err
+
+    N, C, H, W = shape
+    x, w, wds = make(N, C, H, W, 31 + H + C)
+    y, yds = _lib.qconv2d_s2ds(x, w, wds, 4, mode)
+    xn = x.cpu().numpy()
+    ref, _ = O.qconv2d(xn, w.cpu().numpy(), None, 2, 1, 1, 1, 4, mode)
+    refds, _ = O.qconv2d(xn, wds.cpu().numpy(), None, 2, 0, 1, 1, 4, mode)
+    assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL, normwise_err(y.cpu().numpy(), ref)
+    assert normwise_err(yds.cpu().numpy(), refds) <= CONV_TOL, normwise_err(yds.cpu().numpy(), refds)
+
+
+def test_s2ds_epilogues_vs_oracle():
+    """Eval BN + ReLU on conv1 and eval BN on the shortcut, against the oracle."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from tests._util import normwise_err
+
+    for C, W in ((16, 128), (32, 112)):
+        x, w, wds = make(2, C, 8, W, 5 + C)
+        g = torch.Generator().manual_seed(4)
+        ps, psd = (torch.rand(2 * C, generator=g) + 0.5), (torch.rand(2 * C, generator=g) + 0.5)
+        pb, pbd = (torch.randn(2 * C, generator=g) * 0.1), (torch.randn(2 * C, generator=g) * 0.1)
+        y, yds = _lib.qconv2d_s2ds(x, w, wds, 4, "po2", post_scale=ps.to(DEV), post_shift=pb.to(DEV), act="relu",
+                                   post_scale_ds=psd.to(DEV), post_shift_ds=pbd.to(DEV))
+        v = lambda t: t.numpy().astype(np.float64).reshape(1, -1, 1, 1)  # noqa: E731
+        xn = x.cpu().numpy()
+        ref = np.maximum(O.qconv2d(xn, w.cpu().numpy(), None, 2, 1, 1, 1, 4, "po2")[0] * v(ps) + v(pb), 0.0)
+        refds = O.qconv2d(xn, wds.cpu().numpy(), None, 2, 0, 1, 1, 4, "po2")[0] * v(psd) + v(pbd)
+        assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL
+        assert normwise_err(yds.cpu().numpy(), refds) <= CONV_TOL

@@ -36,3 +36,22 @@ def test_split_equals_fused_call(shape, mode):
     assert torch.equal(sc2.conv(x, b), ref)
     with pytest.raises(_lib.Po2qError, match="does not match"):
         sc.conv(torch.randn(N, C, H + 1, W, device=DEV))
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 32, 32, 32, 3, 2, 1), (2, 32, 16, 16, 64, 3, 2, 1)])
+@pytest.mark.parametrize("mode", ["po2", "po2+"])
+def test_split_stride2_transitions(shape, mode):
+    """ResNet56 transition convs (layer2.0 / layer3.0 conv1 @32): the heuristic plan is the stride-2
+    full-row kernel, which only exists with fused weight staging; the split form falls back to a
+    pre-packed plan and still matches the fused call (different kernel: normwise, not bitwise)."""
+    from tests._util import CONV_TOL
+
+    N, C, H, W, K, R, st, pad = shape
+    torch.manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, device=DEV)
+    w = torch.randn(K, C, R, R, device=DEV) * 0.1
+    ref = _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, mode)
+    sc = _lib.SplitConv(x.shape, w, st, pad, 1, 1, 4, mode)
+    sc.pack()
+    y = sc.conv(x)
+    assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL

@@ -36,7 +36,7 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/convtests.log || grep -q "failed\|error" gpurun_out/convtests.log; then
                    echo "stopping: conv GPU tests did not pass"; exit 1
                fi ;;
-        bench) run bench 600 python bench.py --steps 5 --warmup 2 ;;
+        bench) run bench 600 python bench.py ;;
         benchnp) run benchnp 600 python bench.py --steps 5 --warmup 2 --no-pair --no-cpu-baseline ;;
         models) run models_c2 300 python tools/model_bench.py --model resnet56 --image 32 --classes 10 --graph
                 run models_c3 300 python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --graph
@@ -94,10 +94,10 @@ for s in $STEPS; do
                      python3 tools/traffic.py gpurun_out/pmc_trows$i --algorithmic 1644185600 \
                          --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
                  done ;;
-        traffic_pair) run pmc_tpair 300 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" tpair "conv_pair16" hbm
+        traffic_pair) run pmc_tpair 300 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" tpair "conv_pair" hbm
                  cp profiles/traffic.json gpurun_out/traffic.json
                  python3 tools/traffic.py gpurun_out/pmc_tpair --algorithmic 1644274688 --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
-                 run pmc_pair 600 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" pair "conv_pair16" all
+                 run pmc_pair 600 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" pair "conv_pair" all
                  python3 tools/pmc_summary.py gpurun_out/pmc_pair > gpurun_out/pmc_pair_summary.txt 2>&1 ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
@@ -110,7 +110,7 @@ for s in $STEPS; do
         ablate1) run ablate1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 2,3 ;;
         ablate) run ablate 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-                  -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+                  -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cifar ;;
         *) echo "unknown step $s" ;;
     esac
 done
