@@ -205,7 +205,9 @@ int po2q_qconv2d_describe(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K,
  * (utils/quantizers.py:34-36; train.py:79-91 runs loss.backward()):
  *   dw[k][c][r][s] = sum_{n,p,q} dy[n][k][p][q] * x[n][c][p*sh + r*dil_h - pad_h][q*sw + s*dil_w - pad_w]
  * fp32 MFMA (exact products, fp32 accumulation, a fixed summation order: deterministic).
- * groups == 1, R x S in {1x1, 3x3}; PO2Q_ERR_UNSUPPORTED otherwise (the caller falls back).
+ * groups == 1, R x S in {1x1, 3x3}; or depthwise (groups == C == K, the MobileNetV2 / MobileViT
+ * 3x3 depthwise QuantizedConv2d, reference models/mobilenet.py:64-76; R, S <= 5) through an
+ * fp32 per-channel reduction (fixed order); PO2Q_ERR_UNSUPPORTED otherwise (the caller falls back).
  * The input gradient needs no entry of its own: for stride 1 it is po2q_qconv2d_f32 of dy
  * with the weight transposed (K <-> C) and flipped, padding R - 1 - pad (Q is
  * permutation-equivariant, so the same PO2 weights result).
@@ -218,6 +220,16 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw,
                            int64_t stride_h, int64_t stride_w, int64_t pad_h, int64_t pad_w,
                            int64_t dil_h, int64_t dil_w, int64_t groups,
                            void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Zero insertion for strided input gradients (QAT backward, reference train.py:79-91): the input
+ * gradient of a stride-(sh, sw) conv is the stride-1 conv of dy with (s - 1) zeros between its
+ * pixels, with the weight transposed (K <-> C per group) and flipped -- po2q_qconv2d_f32 on the
+ * same PO2 weights.  dst [N, C, Hd, Wd]: dst[n][c][i][j] = src[n][c][i/sh][j/sw] where sh | i,
+ * sw | j and the source pixel exists, else 0.  src [N, C, P, Q].
+ */
+int po2q_dilate_f32(const float* src, float* dst, int64_t N, int64_t C, int64_t P, int64_t Q,
+                    int64_t stride_h, int64_t stride_w, int64_t Hd, int64_t Wd, void* stream);
 
 /*
  * Two chained quantized convs in one launch (ResNet56 stage-1 BasicBlock, reference

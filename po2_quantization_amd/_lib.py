@@ -57,6 +57,7 @@ EXPORTS = (
     "po2q_qconv2d_s2ds_f32",
     "po2q_qconv2d_plan_pack_batch",
     "po2q_qconv2d_plan_run_packed",
+    "po2q_dilate_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -576,7 +577,23 @@ def conv_wgrad(x, gy, wshape, stride=1, padding=0, dilation=1, groups=1):
 
 
 def wgrad_supported(wshape, groups):
-    return int(groups) == 1 and tuple(wshape[2:]) in ((1, 1), (3, 3))
+    """The native weight-gradient kernels cover dense 1x1 / 3x3 layers and depthwise layers
+    (groups == C == K) up to 5x5."""
+    K, Cg, R, S = (int(v) for v in wshape)
+    if int(groups) == 1:
+        return (R, S) in ((1, 1), (3, 3))
+    return Cg == 1 and K == int(groups) and R * S <= 25 and S <= 5
+
+
+def dilate(x, stride, size):
+    """Zero insertion (po2q_dilate_f32): out[n][c][i][j] = x[n][c][i/sh][j/sw] where sh | i and
+    sw | j, else 0; out is [N, C, *size].  The input gradient of a strided conv is the stride-1
+    conv of dilate(dy) with the transposed, flipped weight."""
+    _require_hip_f32(x, "input")
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: dilate needs the operator library (PO2Q_LIB selects another build)")
+    return _op_call(O.dilate, x, list(_pair(stride)), list(_pair(size)))
 
 
 def _plan_choice(key, plan):

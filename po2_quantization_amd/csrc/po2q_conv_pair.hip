@@ -60,14 +60,31 @@ struct PairArgs {
     const float* res;  // RES: residual [N, C, H, W] added before act2
     int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
     int halves;        // C = 16, 1: store 64-byte half lines as the MFMA layout holds them (A/B knob)
+    int stg;           // 1: the stagger (STG) kernel for the forms without a residual
 };
 
-// Channel chunk c4 (channels 4 c4 .. +3, 8 bytes) of pixel P in a shared intermediate
-// plane, XOR-swizzled so the 16 lanes of a ds_write_b64 group (16 pixels, one chunk) cover
-// all 32 banks of its 128-byte window.
+// Byte offset of the 16-byte channel octet `oc` (channels 8 oc .. 8 oc + 7) of pixel P in a
+// shared intermediate plane ([pixel][C] bf16, 2C bytes per pixel), XOR-swizzled at octet
+// granularity: conv 2's A-fragment reads are then ONE conflict-free ds_read_b128 per lane (the
+// four 16-lane groups of that instruction hit 64 distinct banks), and conv 1's epilogue writes
+// (ds_write_b64 of 4 channels, 16 contiguous lanes per group) are 2-way -- against two 2-way
+// ds_read_b64 per fragment with the 8-byte-chunk swizzle this replaces (bank model of
+// MI355X_MICROARCH.md "LDS"; PMC SQ_LDS_BANK_CONFLICT was 35 % of the pair's LDS cycles).
 template <int CC>
-__device__ __forceinline__ int ychunk(int P, int c4) {
-    return P * (2 * CC) + 8 * (c4 ^ ((P >> (CC == 16 ? 2 : 1)) & (CC / 4 - 1)));
+__device__ __forceinline__ int yoct(int P, int oc) {
+    return P * (2 * CC) + 16 * (oc ^ (CC == 16 ? ((P >> 2) & 1) : ((P >> 1) & 3)));
+}
+
+// Byte offset of channel octet `oc` of pixel hp in a wave's x planes.  C = 16: [pixel][16 ch]
+// with the octet XOR-swizzled by (hp >> 2) & 1, so the split's ds_write_b128 (8 contiguous
+// lanes = 8 consecutive pixels) covers all 32 banks and conv 1's fragment reads stay
+// conflict-free (the unswizzled layout made every split write 2-way); C = 32: x_addr.
+template <int CC>
+__device__ __forceinline__ int xa(int hp, int oc) {
+    if constexpr (CC == 16)
+        return hp * 32 + 16 * (oc ^ ((hp >> 2) & 1));
+    else
+        return x_addr<CC>(hp, oc);
 }
 
 // The intermediate h lives in LDS already split: 2 ring slots x 3 planes (hi / mid / lo)
@@ -82,9 +99,18 @@ __device__ __forceinline__ int ychunk(int P, int c4) {
 // E: 0 = plain chain (no bias / affine / activation / residual: y = scale * acc), 1 = the
 // general epilogues (the kernel is bound by vector-instruction issue, so the plain chain
 // skips that work).
-template <int CC, int PD, int NTS, bool RES, int E = 1>
+// STG 1 (stagger, MI355X_MICROARCH "two waves per SIMD" item 9): waves 4.. -- the second wave
+// of each SIMD -- run a step's conv-2 epilogue at the start of the NEXT step and split x row j
+// before their conv-2 MFMAs, so right after the barrier they issue vector work while waves
+// 0-3 issue matrix work, instead of both waves of a SIMD contending for the matrix pipe and
+// then both idling it.  Outputs are bit for bit those of STG 0 (same arithmetic, moved).
+// DBG (diagnostic builds only, -DPO2Q_PAIR_DIAG, PO2Q_PAIR_DEBUG; timing only, outputs are
+// wrong): bit 1 no conv-2 MFMAs, 2 no conv-1 MFMAs, 4 no x DMAs, 8 no output stores, 16 no
+// split / epilogue-1 plane writes.
+template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0>
 __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
+    static_assert(!(STG && RES), "stagger: the residual row's LDS slot is refilled before a deferred epilogue");
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
     constexpr int SW = kQSW<CC>, WC = SW + 2, PL = kQPlane<CC>, KS = kQKS<CC>;
@@ -142,6 +168,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     const uint32_t res_lds = (uint32_t)(uintptr_t)resr;
     // x row jn into raw slot sl; with RES the residual of the output row stored at step jn
     auto load_row = [&](int sl, int jn) __attribute__((always_inline)) {
+        if constexpr ((DBG & 4) != 0) return;
         const int h = p0 - 2 + jn;
         const bool hok = jn < nx && h >= 0 && h < a.H;
         const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
@@ -163,16 +190,16 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     // ---- x split: lane -> (column sc of the strip, channel octet so); halo lanes < 2C ->
     // (side, channel) from the neighbours' columns of the shared raw row (zero outside)
     const int sc = lane % SW, so = lane / SW;
-    const int wa_i = x_addr<CC>(sc + 1, so);
+    const int wa_i = xa<CC>(sc + 1, so);
     const int hside = (lane / CC) & 1, hch = lane % CC;
     const int hq = hside ? q0 + SW : q0 - 1;
     const bool h_ok = lane < 2 * CC && hq >= 0 && hq < a.W;
-    const int wa_h = x_addr<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
+    const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
     const int rdx0 = (so * 8) * (a.Wp * 4) + (q0 + sc) * 4;
     const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
-    // A fragment addresses: x planes (wave-private, pixel = strip column + 1): one b128;
-    // shared intermediate planes (pixel = column + 1): chunks 2o, 2o + 1 of the octet o, two b64
-    int aoff[NG][KS], yoff[NG][KS], yoff2[NG][KS];
+    // A fragment addresses: x planes (wave-private, pixel = strip column + 1) and shared
+    // intermediate planes (pixel = column + 1, swizzled octet o): one b128 each
+    int aoff[NG][KS], yoff[NG][KS];
     {
         const int p = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -193,9 +220,8 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     o = g;
                     zero = false;
                 }
-                aoff[grp][ks] = zero ? zero_off : x_addr<CC>(xp, o);
-                yoff[grp][ks] = zero ? yzero : ychunk<CC>(yp, 2 * o);
-                yoff2[grp][ks] = zero ? yzero + 8 : ychunk<CC>(yp, 2 * o + 1);
+                aoff[grp][ks] = zero ? zero_off : xa<CC>(xp, o);
+                yoff[grp][ks] = zero ? yzero : yoct<CC>(yp, o);
             }
         }
     }
@@ -238,9 +264,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     if constexpr (TR) {
                         af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
                     } else {
-                        const uint2 u0 = *reinterpret_cast<const uint2*>(pb + pl * a.YPL + yoff[grp][ks]);
-                        const uint2 u1 = *reinterpret_cast<const uint2*>(pb + pl * a.YPL + yoff2[grp][ks]);
-                        af[pl][grp] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * a.YPL + yoff[grp][ks]));
                     }
                 }
 #pragma unroll
@@ -266,6 +290,97 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         }
     };
 
+    // conv-2 epilogue of the output row that completes at step j (accumulator slot D of S6)
+    auto epi2 = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S6 = decltype(S_)::value;
+        constexpr int D = (S6 % 3 + 2) % 3;
+        const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
+        const int o = j - 5;
+        const bool orow = o >= 0 && o < rbe;
+        const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
+        const int g = lane >> 4;
+        floatx4 vv[NT][NG];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int ch = 16 * nt + (lane & 15);
+            const uint32_t yrow = (uint32_t)ch * (uint32_t)HW + (uint32_t)(orow ? p0 + o : 0) * a.W;
+#pragma unroll
+            for (int grp = 0; grp < NG; ++grp) {
+                const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
+                floatx4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
+                                  : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                if constexpr (RES) {
+                    const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += r[e];
+                }
+                if constexpr (E != 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
+                }
+                vv[nt][grp] = v;
+                if (CC != 16 || a.halves) {
+                    const int q = q0 + ql;
+                    rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
+                }
+                acc2[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        if (CC == 16 && !a.halves) {
+            // Whole 128-byte lines per store: lane L holds pixels 4g .. 4g + 3 (vv[0][0]) and
+            // 16 + 4g .. (vv[0][1]) of channel L & 15.  One row_ror:8 DPP exchange within each
+            // 16-lane row gives store A channels 0-7 (lanes with bit 3 set take channel L & 7's
+            // second half from lane L - 8) and store B channels 8-15 (lanes without it take
+            // channel 8 + (L & 7)'s first half from lane L + 8): 8 lanes x 16 bytes = one full
+            // line per channel, where two 64-byte halves from two stores cost partial-line
+            // writes (PMC: 1.32x the output bytes with non-temporal stores).
+            const bool hi8 = (lane & 8) != 0;
+            floatx4 sa, sb;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float r1 = __int_as_float(
+                    __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][NG - 1][e]), 0x128, 0xf, 0xf, false));
+                const float r0 = __int_as_float(
+                    __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][0][e]), 0x128, 0xf, 0xf, false));
+                sa[e] = hi8 ? r1 : vv[0][0][e];
+                sb[e] = hi8 ? vv[0][NG - 1][e] : r0;
+            }
+            const int q = q0 + (hi8 ? 16 : 0) + 4 * g;
+            const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
+            const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
+            const bool ok = orow && q < a.W;
+            if constexpr ((DBG & 8) == 0) {
+                rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+                rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+            }
+        }
+    };
+
+    // exact split of x row j (8 channels of one strip column per lane + the halo lanes) into
+    // this wave's planes
+    auto split_x = [&](const uint32_t (&bx)[8], uint32_t hx) __attribute__((always_inline)) {
+        if constexpr ((DBG & 16) != 0) return;
+        uint4 hi, mid, lo;
+        split3(bx, hi, mid, lo);
+        *reinterpret_cast<uint4*>(slab + wa_i) = hi;
+        *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
+        *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
+        if (lane < 2 * CC) {
+            uint16_t h16, m16, l16;
+            split1(h_ok ? hx : 0u, h16, m16, l16);
+            *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+            *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
+            *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
+        }
+    };
+
+    const bool strip_full = q0 + SW <= a.W;  // wave-uniform
+    // the stagger's late waves (wave-uniform: an SGPR branch)
+    const bool late = STG != 0 && wave >= 4;
+
     auto step = [&](auto S_, int j) __attribute__((always_inline)) {
         constexpr int S6 = decltype(S_)::value;
         constexpr int S = S6 % 3;
@@ -284,98 +399,36 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
             for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * (a.Wp * 4));
             hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
         }
+        if constexpr (STG != 0) {
+            if (late) {  // vector work first: the previous step's conv-2 epilogue, then the x split
+                epi2(std::integral_constant<int, (S6 + 5) % 6>{}, j - 1);
+                split_x(bx, hx);
+            }
+        }
 
         // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
-        if (j >= 3) mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
-        {
-            const int o = j - 5;
-            const bool orow = o >= 0 && o < rbe;
-            const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
-            const int g = lane >> 4;
-            floatx4 vv[NT][NG];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int ch = 16 * nt + (lane & 15);
-                const uint32_t yrow = (uint32_t)ch * (uint32_t)HW + (uint32_t)(orow ? p0 + o : 0) * a.W;
-#pragma unroll
-                for (int grp = 0; grp < NG; ++grp) {
-                    const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
-                    floatx4 v;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
-                                      : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
-                    if constexpr (RES) {
-                        const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] += r[e];
-                    }
-                    if constexpr (E != 0) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
-                    }
-                    vv[nt][grp] = v;
-                    if (CC != 16 || a.halves) {
-                        const int q = q0 + ql;
-                        rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
-                    }
-                    acc2[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
-            if (CC == 16 && !a.halves) {
-                // Whole 128-byte lines per store: lane L holds pixels 4g .. 4g + 3 (vv[0][0]) and
-                // 16 + 4g .. (vv[0][1]) of channel L & 15.  One row_ror:8 DPP exchange within each
-                // 16-lane row gives store A channels 0-7 (lanes with bit 3 set take channel L & 7's
-                // second half from lane L - 8) and store B channels 8-15 (lanes without it take
-                // channel 8 + (L & 7)'s first half from lane L + 8): 8 lanes x 16 bytes = one full
-                // line per channel, where two 64-byte halves from two stores cost partial-line
-                // writes (PMC: 1.32x the output bytes with non-temporal stores).
-                const bool hi8 = (lane & 8) != 0;
-                floatx4 sa, sb;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float r1 = __int_as_float(
-                        __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][NG - 1][e]), 0x128, 0xf, 0xf, false));
-                    const float r0 = __int_as_float(
-                        __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][0][e]), 0x128, 0xf, 0xf, false));
-                    sa[e] = hi8 ? r1 : vv[0][0][e];
-                    sb[e] = hi8 ? vv[0][NG - 1][e] : r0;
-                }
-                const int q = q0 + (hi8 ? 16 : 0) + 4 * g;
-                const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
-                const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
-                const bool ok = orow && q < a.W;
-                rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
-                rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
-            }
+        if ((DBG & 1) == 0 && j >= 3)
+            mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
+        if (!late) {
+            epi2(S_, j);
+            split_x(bx, hx);
         }
 
         // ---- conv 1 on x row j (transposed MFMAs); intermediate row i = j - 2 completes
-        {
-            uint4 hi, mid, lo;
-            split3(bx, hi, mid, lo);
-            *reinterpret_cast<uint4*>(slab + wa_i) = hi;
-            *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
-            *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
-            if (lane < 2 * CC) {
-                uint16_t h16, m16, l16;
-                split1(h_ok ? hx : 0u, h16, m16, l16);
-                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
-                *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
-                *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
-            }
-        }
-        mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, bw2, slab);
-        {
+        if constexpr ((DBG & 2) == 0) mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, bw2, slab);
+        if constexpr ((DBG & 16) == 0) {
             const int i = j - 2;
             const int r1 = p0 - 1 + i;
             const bool irow = i >= 0 && i < n1 && r1 >= 0 && r1 < a.H;
             const int p = lane & 15, g = lane >> 4;
             unsigned char* yw = yr + YW * yslot;
+            // wave-uniform: an image row whose every strip column is inside the image needs no
+            // per-value select (the common case: W a multiple of the strip width)
+            const bool allok = irow && strip_full;
 #pragma unroll
             for (int grp = 0; grp < NG; ++grp) {
                 const int q = q0 + 16 * grp + p;  // lane: pixel q, channels 16 nt + 4 g .. + 3
-                const bool ok = irow && q < a.W;
+                const bool ok = allok || (irow && q < a.W);
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     uint32_t b4[4];
@@ -393,7 +446,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     uint16_t h[4], m[4], l[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
-                    const int wo = ychunk<CC>(q + 1, 4 * nt + g);
+                    const int wo = yoct<CC>(q + 1, (4 * nt + g) >> 1) + 8 * (g & 1);
                     *reinterpret_cast<uint2*>(yw + wo) =
                         make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
                     *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
@@ -474,14 +527,20 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     }
     // static priority for the younger wave of each SIMD (MI355X_MICROARCH two-waves item 4)
     if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+    int jl = 0;  // the last step run (its S6 is 2 or 5: both complete accumulator slot 1)
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
         step(std::integral_constant<int, 1>{}, j + 1);
         step(std::integral_constant<int, 2>{}, j + 2);
+        jl = j + 2;
         if (j + 3 >= nsteps) break;
         step(std::integral_constant<int, 3>{}, j + 3);
         step(std::integral_constant<int, 4>{}, j + 4);
         step(std::integral_constant<int, 5>{}, j + 5);
+        jl = j + 5;
+    }
+    if constexpr (STG != 0) {
+        if (late) epi2(std::integral_constant<int, 2>{}, jl);  // the deferred last epilogue
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
 }
@@ -530,10 +589,15 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
                                 hipStream_t s) {
     const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
     const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
-    if (plain)
+    constexpr bool kStg = PD == 2 && NTS == 3;  // the stagger is instantiated for the default ring / store mode
+    if (kStg && plain && a.stg)
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
+    else if (plain)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
     else if (res)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
+    else if (kStg && a.stg)
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
     else
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1>), grid, block, pp.lds, s, x, y, a);
     return hipGetLastError();
@@ -541,11 +605,26 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
 
 static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
                               hipStream_t s) {
+#ifdef PO2Q_PAIR_DIAG
+    if (const char* dv = getenv("PO2Q_PAIR_DEBUG")) {
+        const int dbg = atoi(dv);
+        const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
+#define PO2Q_PD(v) \
+        if (dbg == v && pp.C == 16 && pp.pd == 2 && pp.nts == 3 && !res) { \
+            hipLaunchKernelGGL((conv_pair<16, 2, 3, false, 0, 0, v>), grid, block, pp.lds, s, x, y, a); \
+            return hipGetLastError(); \
+        }
+        PO2Q_PD(1) PO2Q_PD(2) PO2Q_PD(3) PO2Q_PD(4) PO2Q_PD(8) PO2Q_PD(12) PO2Q_PD(16) PO2Q_PD(19)
+        PO2Q_PD(15) PO2Q_PD(31)
+#undef PO2Q_PD
+    }
+#endif
 #define PO2Q_PR(c, d, nt) \
     if (pp.C == c && pp.pd == d && pp.nts == nt) return launch_pair_t<c, d, nt>(pp, a, x, y, res, s);
     PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
     PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
     PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
+    PO2Q_PR(16, 3, 3) PO2Q_PR(16, 4, 3)
 #undef PO2Q_PR
     return hipErrorInvalidValue;
 }
@@ -561,20 +640,24 @@ namespace {
 // non-temporal x loads); default 23: non-temporal
 // loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32 (bs = 256,
 // profiles/r02_pair_nt.log)
-void pair_variant(int& pd, int& nts, int& prio, int& halves, int64_t C) {
+void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C) {
     pd = 2;
     nts = 3;
     // priority 1 for waves 4..: 0.494 vs 0.504 / 0.500 ms at C = 16 (both store modes), mixed at
     // C = 32 (profiles/r02_pair_prio.log)
     prio = C == 16 ? 1 : 0;
     halves = 0;
+    stg = 0;
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
         int v = atoi(e);
+        stg = v >= 10000 ? 1 : 0;  // + 10000: the stagger kernel (STG) where no residual is added
+        v %= 10000;
         halves = v >= 1000 ? 1 : 0;  // + 1000: 64-byte half-line stores (C = 16)
         v %= 1000;
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
-        if ((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) {
+        if (((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) ||
+            (C == 16 && (d == 3 || d == 4) && t == 3)) {
             pd = d;
             nts = t;
         }
@@ -625,8 +708,8 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // the pair is not the faster path, so the advisory says no (the kernel stays callable)
     if (C == 32 && !getenv("PO2Q_PAIR_C32")) return 0;  // PO2Q_PAIR_C32=1: advise it anyway (A/B runs)
     po2q::PairPlan pp;
-    int pd, nts, prio, halves;
-    pair_variant(pd, nts, prio, halves, C);
+    int pd, nts, prio, halves, stg;
+    pair_variant(pd, nts, prio, halves, stg, C);
     return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) &&
                    po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, true, pd, nts)
                ? 1
@@ -647,8 +730,8 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         return PO2Q_ERR_INVALID;
     }
     po2q::PairPlan pp;
-    int pd, nts, prio, halves;
-    pair_variant(pd, nts, prio, halves, C);
+    int pd, nts, prio, halves, stg;
+    pair_variant(pd, nts, prio, halves, stg, C);
     if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, residual != nullptr, pd, nts)) {
         po2q::set_error("po2q: pair: no plan for this shape");
         return PO2Q_ERR_UNSUPPORTED;
@@ -669,6 +752,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.res = residual;
     a.prio = prio;
     a.halves = halves;
+    a.stg = stg;
     const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {
         po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));

@@ -129,15 +129,20 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
 
     // ---- A fragment offsets per k-step (E[p], O[p], E[p+1] for taps 0, 1, 2)
     int aoff[KS];
+    int ads;  // DS: the shortcut's own A fragment -- C = 16: k-step 0 with the tap-0 half read
+              // from the zero slot, so a non-finite tap-0 pixel never meets the B fragment's
+              // zero rows (inf * 0 = NaN where the 1x1 conv never reads that pixel)
     {
         const int p = lane & 15, g = lane >> 4;
         if constexpr (CC == 16) {
             aoff[0] = g < 2 ? x_addr<16>(p, g) : OBASE + x_addr<16>(p, g - 2);
             aoff[1] = g < 2 ? x_addr<16>(p + 1, g) : ZOFF;
+            ads = g < 2 ? ZOFF : aoff[0];
         } else {
             aoff[0] = x_addr<32>(p, g);
             aoff[1] = OBASE + x_addr<32>(p, g);
             aoff[2] = x_addr<32>(p + 1, g);
+            ads = aoff[1];
         }
     }
 
@@ -145,9 +150,6 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * K * PQ, K * PQ * 4);
     constexpr int ST = DS ? 2 * NT : NT;  // stores per step (every step; the idle output's are dropped)
     const __amdgpu_buffer_rsrc_t ryd = rows_rsrc(DS ? a.yds + (int64_t)n * K * PQ : y, DS ? K * PQ * 4 : 4);
-    // DS: the k-step of the A fragment that holds tap (., 1) -- O[p]: k-step 0's upper half
-    // (C = 16, the lower half is tap 0: zero rows in the shortcut's B fragment) or k-step 1
-    constexpr int KDS = CC == 16 ? 0 : 1;
     float scaled = 1.0f;
     bool find = true;
     float epsd[NT], epbd[NT];
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x
             bf16x8 af[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
-                af[pl] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slab + pl * PL + aoff[KDS]));
+                af[pl] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slab + pl * PL + ads));
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 const bf16x8 b = __builtin_bit_cast(bf16x8, wld[nt * 64 + lane]);

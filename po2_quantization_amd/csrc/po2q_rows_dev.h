@@ -78,9 +78,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* p, int b
 // Exact 3-way split of one fp32 value (split3 of po2q_x3_dev.h, one lane value):
 // the bf16 bit patterns of hi / mid / lo.
 __device__ __forceinline__ void split1(uint32_t b, uint16_t& h, uint16_t& m, uint16_t& l) {
-    const float xv = __uint_as_float(b);
-    float r1 = xv - __uint_as_float(b & 0xffff0000u);
-    r1 = __builtin_isinf(xv) ? 0.0f : r1;
+    const float xc = __builtin_amdgcn_fmed3f(__uint_as_float(b), -3.40282347e38f, 3.40282347e38f);
+    const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
     const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
     const uint32_t lb = __float_as_uint(r1 - __uint_as_float(mb));
     h = (uint16_t)(b >> 16);

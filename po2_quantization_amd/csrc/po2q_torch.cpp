@@ -14,7 +14,8 @@
 //   po2q::qconv2d_s2ds   a stage's 3x3 stride-2 conv1 + 1x1 stride-2 shortcut on one read of x
 //                        in one launch: a ResNet56 stage-1 BasicBlock (resnet.py:55-71)
 //   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
-//                        STE, utils/quantizers.py:34-36)
+//                        STE, utils/quantizers.py:34-36), dense and depthwise
+//   po2q::dilate         zero insertion for the strided layers' input gradient
 // Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
 // Errors are TORCH_CHECK -> RuntimeError, as F.conv2d raises for bad arguments.
 #include <ATen/ATen.h>
@@ -267,6 +268,22 @@ at::Tensor conv_wgrad(const at::Tensor& x_, const at::Tensor& dy_, at::IntArrayR
     return gw;
 }
 
+// QAT backward: zero insertion for strided input gradients (po2q_dilate_f32)
+at::Tensor dilate(const at::Tensor& x_, at::IntArrayRef stride, at::IntArrayRef size) {
+    check_hip_f32(x_, "input");
+    TORCH_CHECK(x_.dim() == 4, "po2q: dilate: 4-D input");
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous();
+    const int64_t sh = pick(stride, 0, "stride"), sw = pick(stride, 1, "stride");
+    const int64_t Hd = pick(size, 0, "size"), Wd = pick(size, 1, "size");
+    at::Tensor out = at::empty({x.size(0), x.size(1), Hd, Wd}, x.options());
+    if (out.numel() == 0) return out;
+    const int st = po2q_dilate_f32(x.data_ptr<float>(), out.data_ptr<float>(), x.size(0), x.size(1), x.size(2),
+                                   x.size(3), sh, sw, Hd, Wd, stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return out;
+}
+
 // Two chained 16-channel 3x3 convs in one launch (po2q_qconv2d_pair_f32)
 void check_vec(const c10::optional<at::Tensor>& t, const at::Tensor& x, int64_t n, const char* what) {
     if (!t.has_value()) return;
@@ -392,6 +409,10 @@ at::Tensor qconv2d_fused_meta(const at::Tensor& x, const at::Tensor& w, const c1
 
 at::Tensor same_meta(const at::Tensor& w, int64_t, int64_t, int64_t) { return at::empty_like(w); }
 
+at::Tensor dilate_meta(const at::Tensor& x, at::IntArrayRef, at::IntArrayRef size) {
+    return at::empty({x.size(0), x.size(1), pick(size, 0, "size"), pick(size, 1, "size")}, x.options());
+}
+
 at::Tensor conv_wgrad_meta(const at::Tensor& x, const at::Tensor&, at::IntArrayRef wshape, at::IntArrayRef,
                            at::IntArrayRef, at::IntArrayRef, int64_t) {
     return at::empty(wshape, x.options());
@@ -409,6 +430,7 @@ TORCH_LIBRARY(po2q, m) {
           "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
     m.def("conv_wgrad(Tensor x, Tensor dy, int[] wshape, int[2] stride, int[2] padding, int[2] dilation, "
           "int groups=1) -> Tensor");
+    m.def("dilate(Tensor x, int[2] stride, int[2] size) -> Tensor");
     m.def("qconv2d_pair(Tensor x, Tensor w1, Tensor w2, int bits, int mode, int fsr=1, Tensor? bias1=None, "
           "Tensor? bias2=None, Tensor? post_scale1=None, Tensor? post_shift1=None, int act1=0, "
           "Tensor? post_scale2=None, Tensor? post_shift2=None, Tensor? residual=None, int act2=0) -> Tensor");
@@ -423,6 +445,7 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("qconv2d", &qconv2d);
     m.impl("qconv2d_fused", &qconv2d_fused);
     m.impl("conv_wgrad", &conv_wgrad);
+    m.impl("dilate", &dilate);
     m.impl("qconv2d_pair", &qconv2d_pair);
     m.impl("qconv2d_s2ds", &qconv2d_s2ds);
 }
@@ -433,6 +456,7 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("qconv2d", &qconv2d_meta);
     m.impl("qconv2d_fused", &qconv2d_fused_meta);
     m.impl("conv_wgrad", &conv_wgrad_meta);
+    m.impl("dilate", &dilate_meta);
     m.impl("qconv2d_pair", &qconv2d_pair_meta);
     m.impl("qconv2d_s2ds", &qconv2d_s2ds_meta);
 }

@@ -552,9 +552,22 @@ Wgrad2Choice wgrad2_choose(const po2q::WgradArgs& a1) {
 
 }  // namespace
 
+// depthwise layers (groups == C == K): po2q_bwd.hip
+size_t po2q_dw_wgrad_workspace_bytes_internal(int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
+                                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
+                                              int64_t dw);
+int po2q_dw_wgrad_f32_internal(const float* x, const float* dy, float* dwt, int64_t N, int64_t C, int64_t H,
+                               int64_t W, int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                               int64_t dh, int64_t dw, void* workspace, size_t workspace_bytes, void* stream);
+
+static bool wgrad_depthwise(int64_t C, int64_t K, int64_t groups) { return groups > 1 && groups == C && K == C; }
+
 size_t po2q_qconv2d_wgrad_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R,
                                           int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
                                           int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups) {
+    if (wgrad_depthwise(C, K, groups))
+        return po2q_dw_wgrad_workspace_bytes_internal(N, C, H, W, R, S, stride_h, stride_w, pad_h, pad_w, dil_h,
+                                                      dil_w);
     po2q::WgradArgs a;
     size_t lds, part;
     if (!wgrad_setup(a, lds, part, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups))
@@ -567,6 +580,9 @@ int po2q_qconv2d_wgrad_f32(const float* x, const float* dy, float* dw, int64_t N
                            int64_t K, int64_t R, int64_t S, int64_t stride_h, int64_t stride_w, int64_t pad_h,
                            int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t groups, void* workspace,
                            size_t workspace_bytes, void* stream) {
+    if (wgrad_depthwise(C, K, groups))
+        return po2q_dw_wgrad_f32_internal(x, dy, dw, N, C, H, W, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w,
+                                          workspace, workspace_bytes, stream);
     po2q::WgradArgs a;
     size_t lds, part;
     if (!wgrad_setup(a, lds, part, N, C, H, W, K, R, S, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups))

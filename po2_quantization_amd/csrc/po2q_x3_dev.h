@@ -31,16 +31,18 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // Exact 3-way bf16 split of 8 fp32 values (bit patterns):
 //   hi = x & 0xffff0000, r1 = x - hi (exact), mid = r1 & 0xffff0000, lo = r1 - mid.
-// NaN needs no care (r1 = NaN, so mid/lo are NaN and so is every product sum).
+// NaN needs no care (hi is NaN, and so is every product sum).
 // +-inf would give r1 = inf - inf = NaN where the reference's product is +-inf, so
-// r1 is forced to 0 there (v_cmp_class + v_cndmask: branch-free, no exec juggling).
+// r1 comes from the value clamped to +-FLT_MAX (v_med3: identity on every finite value):
+// hi keeps +-inf, mid / lo are finite, and the products sum to +-inf as the reference's do.
 __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
     uint32_t mb[8], lb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float xv = __uint_as_float(b[j]);
-        float r1 = xv - __uint_as_float(b[j] & 0xffff0000u);
-        r1 = __builtin_isinf(xv) ? 0.0f : r1;
+        // +-inf: r1 from the value clamped to +-FLT_MAX (one v_med3 instead of a class test and
+        // a select): finite mid / lo beside hi = +-inf, so every product sum stays +-inf
+        const float xc = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
+        const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
         mb[j] = __float_as_uint(r1) & 0xffff0000u;
         lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
     }

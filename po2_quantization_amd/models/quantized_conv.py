@@ -13,8 +13,8 @@ same get_quantization_error().  forward() runs the fused libpo2q path:
 
 Backward (QAT) keeps the reference's semantics: straight-through estimator on
 the weight (quantizers.py:34-36), conv gradients of the quantized weight -- the input
-gradient of stride-1 layers through the native bf16x3 conv kernels, the weight gradient
-through the native fp32-MFMA wgrad kernel (_QConv2dFn.backward).
+gradient through the native conv kernels (strided layers on zero-inserted dy), the weight
+gradient through the native fp32 wgrad kernels, dense and depthwise (_QConv2dFn.backward).
 Inputs must be fp32 HIP tensors; there is no CPU path.
 
 Inference fusion: `fused(x, bn=, act=, residual=)` runs the conv
@@ -33,6 +33,9 @@ from ..utils.quantizers import NATIVE_MODES
 
 # False: every backward is one aten.convolution_backward of Q(w) (for A/B measurements)
 NATIVE_BACKWARD = True
+# backward calls that needed aten.convolution_backward for part of their gradients (tests
+# assert it stays 0 on the reference models' layers)
+ATEN_BACKWARD_CALLS = 0
 
 
 class _QConv2dFn(torch.autograd.Function):
@@ -47,35 +50,46 @@ class _QConv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         """The gradients autograd takes through F.conv2d(x, Q(w), bias) with the straight-
-        through estimator on Q (quantizers.py:34-36; train.py:79-91), natively where the
-        kernels cover the layer:
-          input  -- stride 1, dilation 1, groups 1: the fused quantize + conv of gy with the
-                    weight transposed (K <-> C) and flipped, padding R-1-p: Q commutes with
-                    that permutation, so these are the same exact PO2 weights (bf16x3);
-          weight -- groups 1, 1x1 / 3x3: po2q_qconv2d_wgrad_f32 (fp32 MFMA);
+        through estimator on Q (quantizers.py:34-36; train.py:79-91), natively:
+          input  -- the fused quantize + conv of gy (stride 1) or of gy with stride - 1 zeros
+                    inserted between its pixels (po2q_dilate_f32; strided layers) with the
+                    weight transposed (K <-> C within each group) and flipped, padding
+                    dil * (R - 1) - pad: Q commutes with that permutation, so these are the same
+                    exact PO2 weights; dense, grouped and depthwise layers alike;
+          weight -- po2q_qconv2d_wgrad_f32: fp32 MFMA for dense 1x1 / 3x3 layers, a fixed-order
+                    fp32 reduction for depthwise layers;
           bias   -- sum of gy over N, P, Q.
-        Anything else (stride-2 input gradients, grouped / depthwise layers) is issued as one
-        aten.convolution_backward of Q(w), as autograd would."""
+        What no kernel covers (padding beyond dil * (R - 1), grouped non-depthwise weight
+        gradients, other kernel sizes) is issued as one aten.convolution_backward of Q(w)."""
         x, weight, bias = ctx.saved_tensors
         stride, padding, dilation, groups, bits, mode = ctx.conf
         gy = gy.contiguous()
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_b = bias is not None and ctx.needs_input_grad[2]
-        R, S = weight.shape[2], weight.shape[3]
-        pad = _lib._pair(padding)
-        native_x = (NATIVE_BACKWARD and need_x and tuple(_lib._pair(stride)) == (1, 1) and tuple(_lib._pair(dilation)) == (1, 1)
-                    and groups == 1 and pad[0] <= R - 1 and pad[1] <= S - 1)
+        K, Cg, R, S = weight.shape
+        st, pad, dil = _lib._pair(stride), _lib._pair(padding), _lib._pair(dilation)
+        padl = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
+        native_x = NATIVE_BACKWARD and need_x and padl[0] >= 0 and padl[1] >= 0
         native_w = NATIVE_BACKWARD and need_w and _lib.wgrad_supported(weight.shape, groups)
         gx = gw = gb = None
         if native_x:
-            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
-            gx = _lib.qconv2d(gy, wt, None, 1, (R - 1 - pad[0], S - 1 - pad[1]), 1, 1, bits, mode, 1, ctx.precision)
+            G = int(groups)
+            wt = weight.detach().view(G, K // G, Cg, R, S).transpose(1, 2).reshape(G * Cg, K // G, R, S)
+            wt = wt.flip(2, 3).contiguous()
+            src = gy
+            if tuple(st) != (1, 1):
+                H, W = x.shape[2], x.shape[3]
+                size = (H + 2 * pad[0] - dil[0] * (R - 1), W + 2 * pad[1] - dil[1] * (S - 1))
+                src = _lib.dilate(gy, st, size)
+            gx = _lib.qconv2d(src, wt, None, 1, padl, dil, G, bits, mode, 1, ctx.precision)
         if native_w:
             gw = _lib.conv_wgrad(x, gy, weight.shape, stride, padding, dilation, groups)
         if need_b:
             gb = gy.sum(dim=(0, 2, 3))
         rest_x, rest_w = need_x and not native_x, need_w and not native_w
         if rest_x or rest_w:
+            global ATEN_BACKWARD_CALLS
+            ATEN_BACKWARD_CALLS += 1
             qw = weight if mode == "none" else _lib.quantize(weight, bits, mode)
             rx, rw, _ = torch.ops.aten.convolution_backward(
                 gy, x, qw, None, list(stride), list(padding), list(dilation), False, [0, 0], groups,

@@ -19,11 +19,11 @@ def nerr(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
 
 
-def ref_grads(x, w, b, gy, qn, bits, stride, pad):
+def ref_grads(x, w, b, gy, qn, bits, stride, pad, groups=1, dil=1):
     qw = w if qn is None else _lib.quantize(w, bits, qn)
     gx, gw, gb = torch.ops.aten.convolution_backward(
         gy.double().cpu(), x.double().cpu(), qw.double().cpu(), None if b is None else [b.shape[0]],
-        [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1, [True, True, b is not None])
+        [stride, stride], [pad, pad], [dil, dil], False, [0, 0], groups, [True, True, b is not None])
     return gx, gw, gb
 
 
@@ -31,7 +31,7 @@ SHAPES = [  # N, C, H, W, K, R, stride, pad, bias, quantizer
     (2, 16, 20, 20, 16, 3, 1, 1, False, "po2"),
     (2, 32, 12, 12, 32, 3, 1, 1, False, "po2+"),
     (1, 64, 10, 10, 64, 3, 1, 1, True, "po2"),
-    (2, 16, 17, 17, 32, 3, 2, 1, False, "po2"),    # stride 2: input grad via aten, weight grad native
+    (2, 16, 17, 17, 32, 3, 2, 1, False, "po2"),    # stride 2: input grad on zero-inserted dy
     (2, 16, 16, 16, 32, 1, 2, 0, False, "po2+"),   # 1x1 projection
     (1, 8, 9, 70, 24, 3, 1, 1, True, "po2"),       # ragged channels / columns
     (3, 16, 8, 8, 16, 3, 1, 1, False, None),       # plain conv (quantize_fn None)
@@ -137,3 +137,86 @@ def test_wgrad_kernels_vs_torch_fp64(shape):
                                                    None, [st, st], [pad, pad], [dil, dil], False, [0, 0], 1,
                                                    [False, True, False])
     assert nerr(gw, rw) <= CONV_TOL, nerr(gw, rw)
+
+
+GROUPED = [  # N, C, H, W, K, R, stride, pad, dilation, groups, quantizer
+    (2, 32, 16, 16, 32, 3, 1, 1, 1, 32, "po2+"),   # MobileNetV2 depthwise, stride 1
+    (2, 96, 17, 17, 96, 3, 2, 1, 1, 96, "po2+"),   # depthwise stride 2, odd size
+    (3, 144, 8, 8, 144, 3, 2, 1, 1, 144, "po2"),   # depthwise stride 2, even size
+    (1, 24, 9, 13, 24, 5, 1, 2, 1, 24, "po2"),     # depthwise 5x5
+    (2, 16, 12, 12, 32, 3, 1, 1, 1, 2, "po2"),     # grouped (input grad native, weight grad aten)
+    (2, 16, 15, 15, 32, 3, 2, 1, 1, 1, "po2+"),    # dense stride 2, odd size
+    (2, 8, 12, 12, 8, 3, 1, 2, 2, 1, "po2"),       # dilation 2
+    (2, 16, 16, 16, 32, 1, 2, 0, 1, 1, None),      # 1x1 stride 2, plain weights
+]
+
+
+@pytest.mark.parametrize("shape", GROUPED, ids=[str(s) for s in GROUPED])
+def test_grouped_strided_backward_vs_torch_fp64(shape):
+    """Depthwise / grouped / strided / dilated layers: the input gradient through the forward
+    kernels on zero-inserted dy, the depthwise weight gradient through its own kernel; against
+    torch's fp64 CPU convolution_backward of Q(w).  Native unless marked (grouped non-depthwise
+    weight gradients)."""
+    from po2_quantization_amd.models import quantized_conv as qc
+
+    N, C, H, W, K, R, st, pad, dil, groups, qn = shape
+    g = torch.Generator().manual_seed(N * 7 + C + K + R)
+    conv = QuantizedConv2d(C, K, R, stride=st, padding=pad, dilation=dil, groups=groups,
+                           quantize_fn=quantizer_dict[qn] if qn else None, bits=4)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.3)
+    conv = conv.to(DEV)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV).requires_grad_(True)
+    before = qc.ATEN_BACKWARD_CALLS
+    y = conv(x)
+    gy = torch.randn(y.shape, generator=g).to(DEV)
+    y.backward(gy)
+    rx, rw, _ = ref_grads(x.detach(), conv.weight.detach(), None, gy, qn, 4, st, pad, groups, dil)
+    assert nerr(x.grad, rx) <= CONV_TOL, nerr(x.grad, rx)
+    assert nerr(conv.weight.grad, rw) <= CONV_TOL, nerr(conv.weight.grad, rw)
+    dense_or_dw = groups == 1 or (groups == C == K)
+    assert (qc.ATEN_BACKWARD_CALLS == before) == dense_or_dw
+
+
+def test_reference_models_backward_all_native():
+    """One QAT backward of ResNet20 and MobileNetV2 (CIFAR, po2+ 4-bit): no layer falls back to
+    aten.convolution_backward (reference train.py:79-91)."""
+    from po2_quantization_amd.models import quantized_conv as qc
+    from po2_quantization_amd.models.model import get_model
+
+    for mt in ("resnet20", "mobilenet"):
+        m = get_model(mt, 10, quantizer_dict["po2+"], 4, (32, 32)).to(DEV).train()
+        x = torch.randn(8, 3, 32, 32, device=DEV)
+        before = qc.ATEN_BACKWARD_CALLS
+        m(x).sum().backward()
+        assert qc.ATEN_BACKWARD_CALLS == before, mt
+
+
+@pytest.mark.parametrize("C,H,st", [(96, 32, 1), (144, 16, 2), (960, 4, 1)])
+def test_depthwise_wgrad_full_size_vs_torch(C, H, st):
+    """MobileNetV2 @32 depthwise layers at bs = 256: the depthwise weight gradient and the input
+    gradient against torch's fp32 GPU convolution_backward of Q(w)."""
+    torch.manual_seed(C)
+    x = torch.randn(256, C, H, H, device=DEV)
+    w = torch.randn(C, 1, 3, 3, device=DEV) * 0.3
+    P = (H + 2 - 3) // st + 1
+    gy = torch.randn(256, C, P, P, device=DEV)
+    gw = _lib.conv_wgrad(x, gy, w.shape, st, 1, 1, C)
+    qw = _lib.quantize(w, 4, "po2+")
+    rx, rw, _ = torch.ops.aten.convolution_backward(gy, x, qw, None, [st, st], [1, 1], [1, 1], False, [0, 0], C,
+                                                     [True, True, False])
+    assert nerr(gw, rw) <= CONV_TOL, nerr(gw, rw)
+    src = gy if st == 1 else _lib.dilate(gy, st, (H + 2 - 2, H + 2 - 2))
+    gx = _lib.qconv2d(src, w.flip(2, 3).contiguous(), None, 1, 1, 1, C, 4, "po2+")
+    assert nerr(gx, rx) <= CONV_TOL, nerr(gx, rx)
+
+
+def test_dilate_zero_insertion():
+    x = torch.randn(2, 3, 5, 4, device=DEV)
+    for st, size in (((2, 2), (9, 7)), ((2, 3), (10, 11)), ((1, 1), (5, 4))):
+        y = _lib.dilate(x, st, size)
+        ref = torch.zeros(2, 3, *size, device=DEV)
+        sub = ref[:, :, ::st[0], ::st[1]]
+        h, w = min(sub.shape[2], 5), min(sub.shape[3], 4)
+        ref[:, :, :h * st[0]:st[0], :w * st[1]:st[1]] = x[:, :, :h, :w]
+        assert torch.equal(y, ref), st

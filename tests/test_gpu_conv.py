@@ -349,3 +349,73 @@ def test_fused_epilogue_every_candidate_plan(shape, monkeypatch):
             y = _lib.qconv2d_fused(x, w, None, 1, 1, post_scale=ps, post_shift=pb, residual=r, act=act)
             err = ((y - ref).abs().max() / ref.abs().max()).item()
             assert err <= CONV_TOL, (i, act, err)
+
+
+NONFINITE_SHAPES = [(2, 16, 12, 224, 16, 3, 1, 1), (2, 32, 10, 112, 32, 3, 1, 1), (2, 64, 9, 56, 64, 3, 1, 1),
+                    (2, 16, 11, 64, 32, 3, 2, 1), (2, 32, 8, 32, 64, 1, 2, 0), (2, 24, 6, 6, 144, 1, 1, 0)]
+
+
+def _nonfinite_input(N, C, H, W, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, C, H, W, generator=g)
+    flat = x.view(-1)
+    idx = torch.randperm(flat.numel(), generator=g)[:6]
+    sig = torch.tensor([0x7F800001], dtype=torch.int32).view(torch.float32)  # signaling NaN, low payload only
+    for v, i in zip((float("inf"), float("-inf"), float("nan"), float("inf"), sig.item(), float("-inf")), idx):
+        flat[i] = v
+    return x
+
+
+def _same_nonfinite(y, ref):
+    return (torch.equal(torch.isnan(y), torch.isnan(ref)) and torch.equal(torch.isposinf(y), torch.isposinf(ref))
+            and torch.equal(torch.isneginf(y), torch.isneginf(ref)))
+
+
+def _oracle_ref(x, w, st, pad, mode="po2"):
+    """fp64 direct conv of Q(w) (the oracle): the mathematical non-finite pattern (a Winograd or
+    FFT conv, as MIOpen may pick for torch's own conv, can turn +-inf into NaN)."""
+    y, _ = O.qconv2d(x.cpu().numpy(), w.cpu().numpy(), None, st, pad, 1, 1, 4, mode)
+    return torch.from_numpy(y).float()
+
+
+@pytest.mark.parametrize("shape", NONFINITE_SHAPES, ids=[str(s) for s in NONFINITE_SHAPES])
+def test_nonfinite_inputs_every_plan_match_oracle(shape):
+    """+-inf and NaN activations (incl. a signaling NaN whose payload sits in the low 16 bits):
+    every candidate plan reproduces the direct conv's NaN / +-inf pattern exactly (the bf16x3
+    split clamps to +-FLT_MAX for mid / lo, hi keeps the non-finite value), finite outputs at
+    the parity bar."""
+    N, C, H, W, K, R, st, pad = shape
+    x = _nonfinite_input(N, C, H, W, sum(shape)).to(DEV)
+    g = torch.Generator().manual_seed(3)
+    w = (torch.randn(K, C, R, R, generator=g) * 0.2).to(DEV)
+    ref = _oracle_ref(x, w, st, pad)
+    fin = torch.isfinite(ref)
+    assert (~fin).any()
+    bad = []
+    for i, desc in enumerate(_lib.plans(N, C, H, W, K, R, R, st, pad)):
+        y = _lib.qconv2d(x, w, None, st, pad, 1, 1, 4, "po2", plan=i).cpu()
+        if not _same_nonfinite(y, ref):
+            bad.append((i, desc.split(" tile")[0], int((torch.isnan(y) != torch.isnan(ref)).sum()),
+                        int((torch.isinf(y) != torch.isinf(ref)).sum())))
+            continue
+        err = ((y[fin] - ref[fin]).abs().max() / ref[fin].abs().max()).item()
+        assert err <= CONV_TOL, (desc, err)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("C,W", [(16, 224), (32, 112)])
+def test_nonfinite_inputs_pair_and_s2ds(C, W):
+    """The fused-block kernels keep the same non-finite pattern as the module sequence."""
+    import torch.nn.functional as F
+
+    x = _nonfinite_input(2, C, 10, W, C + W).to(DEV)
+    g = torch.Generator().manual_seed(5)
+    w1, w2 = (torch.randn(C, C, 3, 3, generator=g) * 0.1).to(DEV), (torch.randn(C, C, 3, 3, generator=g) * 0.1).to(DEV)
+    y = _lib.qconv2d_pair(x, w1, w2, 4, "po2").cpu()
+    h = _oracle_ref(x, w1, 1, 1)
+    assert _same_nonfinite(y, _oracle_ref(h, w2, 1, 1))
+    wd = (torch.randn(2 * C, C, 1, 1, generator=g) * 0.2).to(DEV)
+    w3 = (torch.randn(2 * C, C, 3, 3, generator=g) * 0.1).to(DEV)
+    y3, yd = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2")
+    assert _same_nonfinite(y3.cpu(), _oracle_ref(x, w3, 2, 1))
+    assert _same_nonfinite(yd.cpu(), _oracle_ref(x, wd, 2, 0))

@@ -57,6 +57,14 @@ for s in $STEPS; do
                    echo "stopping: pair GPU tests did not pass"; exit 1
                fi ;;
         pairb) run pairb 300 python tools/pair_bench.py ;;
+        pairstg) run pairstg 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123,10023,23 python tools/pair_bench.py ;;
+        pairablate) run pairablate 300 python tools/pair_ablate.py ;;
+        pairpd) run pairpd 300 env PAIR_C32=0 PAIR_VARIANTS=23,33,43,123,133,143 python tools/pair_bench.py ;;
+        pairq) run pairq 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123 python tools/pair_bench.py ;;
+        benchq) run benchq 300 python bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-cifar ;;
+        abstg) for r in 1 2; do for v in 123 10123 10023; do
+                   run abstg_${v}_$r 300 env PO2Q_PAIR_VARIANT=$v python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
+               done; done ;;
         modeltests) run modeltests 600 python -u -m pytest tests/test_gpu_models.py -m gpu -x -q --timeout 300 --timeout-method thread
                if ! grep -q " passed" gpurun_out/modeltests.log || grep -q "failed\|error" gpurun_out/modeltests.log; then
                    echo "stopping: model GPU tests did not pass"; exit 1

@@ -19,7 +19,9 @@ def main():
     N = int(os.environ.get("PAIR_N", "256"))
     dev = torch.device("cuda:0")
     _lib.benchmark = True
-    for C, H in ((16, 224), (32, 112)):  # ResNet56 @224 stage 1 and stage 2
+    variants = os.environ.get("PAIR_VARIANTS", "23,123,20,120").split(",")
+    shapes = ((16, 224), (32, 112)) if os.environ.get("PAIR_C32", "1") == "1" else ((16, 224),)
+    for C, H in shapes:  # ResNet56 @224 stage 1 and stage 2
         x = torch.relu(torch.randn(N, C, H, H, device=dev))
         w1 = torch.randn(C, C, 3, 3, device=dev) * 0.1
         w2 = torch.randn(C, C, 3, 3, device=dev) * 0.1
@@ -27,7 +29,7 @@ def main():
         nbytes = 4.0 * (2 * N * C * H * H + 4 * C * C * 9)
         res = {}
         for rnd in range(3):
-            for v in ("23", "123", "20", "120"):
+            for v in variants:
                 os.environ["PO2Q_PAIR_VARIANT"] = v
                 res.setdefault("pair_" + v, []).append(timeit(lambda: _lib.qconv2d_pair(x, w1, w2, 4, "po2"), 11))
             res.setdefault("two_convs", []).append(
