@@ -113,8 +113,7 @@ struct WsLayout {
 static WsLayout ws_layout(const ConvPlan& p, int mode) {
     WsLayout L;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
-    const bool fused = (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS ||
-                        p.kind == KIND_DEPTHWISE) &&
+    const bool fused = (is_bf16x3_kind(p.kind) || p.kind == KIND_DEPTHWISE) &&
                        nw <= kFusedAbsmaxMax;
     L.nparts = (mode == PO2Q_MODE_NONE || fused) ? 0 : absmax_blocks(nw);
     L.part_bytes = align_up((size_t)absmax_blocks(nw) * sizeof(unsigned));
@@ -181,11 +180,15 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     void* packed = ws + L.packed_off;
     const int64_t nw = (int64_t)p.K * p.Cg * p.R * p.S;
     int st;
+    if (p.kind == KIND_DIRECT_F32 || p.kind == KIND_PW_F32) {  // mode none: the weight as given, no pack
+        if (!(phases & RUN_CONV)) return PO2Q_OK;
+        return hip_status(launch_conv_f32s(p, x, w, bias, y, e.ps, e.pb, e.res, e.act, s), "conv launch");
+    }
     if ((phases & RUN_PACK) && L.nparts > 0) {
         st = hip_status(launch_absmax(w, nw, partial, L.nparts, s), "absmax launch");
         if (st) return st;
     }
-    if (p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS) {
+    if (is_bf16x3_kind(p.kind)) {
         // fused weight staging (row plans with fp): the conv quantizes + packs the weight
         // itself -- one launch, nothing in the workspace
         WQuant q;
@@ -206,6 +209,8 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         }
         if (!(phases & RUN_CONV)) return PO2Q_OK;
         const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
+        if (p.kind == KIND_BF16X3_PW)  // affine, residual and activation all in the kernel's stores
+            return hip_status(launch_conv_pw(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s), "conv launch");
         hipError_t he;
         bool fused_affine = false;
         if (p.kind == KIND_BF16X3_DMA) {
@@ -244,7 +249,8 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, false, s), "epilogue launch");
 }
 
-static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows"};
+static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows", "bf16x3_pw",
+                                   "direct_f32", "pw_f32"};
 
 static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
     snprintf(buf, len,
@@ -574,7 +580,7 @@ int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, cons
             set_error("po2q: pack batch: workspace too small (need " + std::to_string(L.total) + " bytes)");
             return PO2Q_ERR_WORKSPACE;
         }
-        const bool x3 = p.kind == KIND_BF16X3 || p.kind == KIND_BF16X3_DMA || p.kind == KIND_BF16X3_ROWS;
+        const bool x3 = is_bf16x3_kind(p.kind);
         if (x3 && p.fp) continue;  // the conv stages its own weight
         const bool batchable = x3 && L.nparts == 0 && (bp.empty() || (h->bits == bits && h->fsr == fsr && h->mode == mode));
         if (!batchable) {  // its own pack launch(es), as po2q_qconv2d_pack_f32

@@ -265,7 +265,22 @@ static bool plan_fallback(ConvPlan& p, bool dw3 = true);
 
 // Heuristic plan + the ranked bf16x3 alternatives (empty unless bf16x3 applies).
 static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, std::vector<PlanCand>* reg_out,
-                           std::vector<PlanCand>* dma_out, std::vector<PlanCand>* rows_out = nullptr) {
+                           std::vector<PlanCand>* dma_out, std::vector<PlanCand>* rows_out = nullptr,
+                           std::vector<PlanCand>* pw_out = nullptr) {
+    if (mode == 0 && flags != 2) {
+        // unquantized weights: the direct stem kernel / the fp32 pointwise GEMM where they apply,
+        // the generic fp32 MFMA kernel as the autotuner's alternative
+        std::vector<PlanCand> f32;
+        f32s_candidates(p, f32);
+        if (!f32.empty()) {
+            PlanCand fb{1e30, p};
+            const bool fb_ok = plan_fallback(fb.plan);
+            if (fb_ok) f32.push_back(fb);
+            p = f32[0].plan;
+            if (pw_out) *pw_out = std::move(f32);
+            return true;
+        }
+    }
     if (bf16x3_wanted(p, mode, flags)) {
         std::vector<PlanCand> reg, dma;
         x3_candidates(p, mode, bits, fsr, reg);
@@ -280,6 +295,11 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
             // the row-streaming kernels beat both tile kernels on every shape they take
             // (profiles/r01_v9_plan_sweep.jsonl, r01_v10_plan_sweep.jsonl)
             if (!rows.empty() && !tuning_knobs()) p = rows[0].plan;
+            // 1x1 / stride 1: the pointwise GEMM kernel (no halo, no LDS, fused epilogue)
+            std::vector<PlanCand> pwc;
+            pw_candidates(p, mode, bits, fsr, pwc);
+            if (!pwc.empty() && !tuning_knobs()) p = pwc[0].plan;
+            if (pw_out) *pw_out = std::move(pwc);
             if (rows_out) *rows_out = std::move(rows);
             if (reg_out) *reg_out = std::move(reg);
             if (dma_out) *dma_out = std::move(dma);
@@ -322,8 +342,8 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
                      int64_t groups, int mode, int bits, int fsr, int flags) {
     ConvPlan p;
     if (!plan_geometry(p, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups)) return false;
-    std::vector<PlanCand> reg, dma, rows;
-    if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma, &rows)) return false;
+    std::vector<PlanCand> reg, dma, rows, pwc;
+    if (!plan_heuristic(p, mode, bits, fsr, flags, &reg, &dma, &rows, &pwc)) return false;
     out.clear();
     out.push_back(p);
     if (p.kind == KIND_DEPTHWISE && p.vrx == 1) {  // the one-output-per-lane kernel as the alternative
@@ -343,6 +363,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             if (!dup) out.push_back(c);
         }
     };
+    add(pwc, 3);
     add(rows, kTuneRowsCands);
     add(reg, kTuneRegCands);
     add(dma, kTuneDmaCands);

@@ -1,0 +1,301 @@
+// fp32 convs for the layers the reference leaves UNQUANTIZED (plain nn.Conv2d with fp32
+// weights; also any QuantizedConv2d whose quantizer is not po2 / po2+, which reaches the native
+// conv as mode "none" with the quantized weight), with the eval BatchNorm / activation /
+// residual of the block in the store:
+//
+//  * conv_direct_f32 -- the 3-input-channel stems: ResNet's conv1 3 -> 16 3x3 s1 (reference
+//    models/resnet.py:99-102, 191), MobileNetV2's features[0] 3 -> 32 3x3 s2
+//    (models/mobilenet.py:41-46, 167), MobileViT's conv1 3 -> 16 3x3 s2 (models/mobile_vit.py:
+//    41-48, 456).  27 MACs per output: a direct VALU conv (fp32 fma, weights wave-uniform), one
+//    thread = 4 consecutive output pixels x 16 output channels; bound by the output write
+//    (16 channels per input pixel);
+//  * conv_pw_f32 -- unquantized 1x1 convs (MobileNetV2's last conv 320 -> 1280,
+//    models/mobilenet.py:185; MobileViT's to_logits conv): the pointwise GEMM of
+//    po2q_conv_pw.hip on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "../../include/po2q.h"
+#include "po2q_epi.h"
+#include "po2q_internal.h"
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+struct F32sArgs {
+    int N, C, H, W, K, P, Q, ph, pw;
+    int KB;           // direct: output channels per thread (16); pw: tiles per wave (NJ)
+    int items;        // direct: threads with work (N x P x ceil(Q / 4)); pw: wave items
+    int Q4, NT, PG;
+    int64_t M;        // pw: N * P * Q pixels
+    const float* ps;  // eval BN affine (NULL: none)
+    const float* pb;
+    const float* res;  // residual [N, K, P, Q] (NULL: none)
+    int act;
+};
+
+__device__ __forceinline__ void f32s_store4(const F32sArgs& a, float* __restrict__ y, int n, int k, int p, int q,
+                                            float (&v)[4], const float* __restrict__ bias, bool epi) {
+    const float bk = bias ? bias[k] : 0.0f;
+    const float s = (epi && a.ps) ? a.ps[k] : 1.0f;
+    const float t = (epi && a.pb) ? a.pb[k] : 0.0f;
+    const int64_t off = (((int64_t)n * a.K + k) * a.P + p) * a.Q + q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        v[e] += bk;
+        if (epi) v[e] = v[e] * s + t;
+    }
+    if ((a.Q & 3) == 0) {  // q is a multiple of 4: one aligned float4
+        if (epi && a.res) {
+            const float4 r = *reinterpret_cast<const float4*>(a.res + off);
+            v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        if (epi) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act);
+        }
+        *reinterpret_cast<float4*>(y + off) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (q + e >= a.Q) break;
+            float u = v[e];
+            if (epi && a.res) u += a.res[off + e];
+            if (epi) u = epi_act(u, a.act);
+            y[off + e] = u;
+        }
+    }
+}
+
+// Direct 3x3 conv, C <= 4 input channels, stride SH, pad (ph, pw): thread = (image n, output
+// row p, 4 output columns q0 .. q0 + 3) x the 16 output channels of blockIdx.y.
+template <int SH, int CMAX>
+__global__ __launch_bounds__(256) void conv_direct_f32(const float* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ y,
+                                                       F32sArgs a, int epi) {
+    constexpr int IC = (4 - 1) * SH + 3;  // input columns the 4 outputs touch
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= a.items) return;
+    const int k0 = (int)blockIdx.y * 16;
+    const int q4 = t % a.Q4;
+    const int rest = t / a.Q4;
+    const int p = rest % a.P, n = rest / a.P;
+    const int q0 = 4 * q4;
+    // input window: rows p*SH - ph + r, columns q0*SH - pw + j, j < IC
+    float xv[CMAX][3][IC];
+    const int h0 = p * SH - a.ph, w0 = q0 * SH - a.pw;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int h = h0 + r;
+            const bool hok = c < a.C && h >= 0 && h < a.H;
+            const float* row = x + (((int64_t)n * a.C + (c < a.C ? c : 0)) * a.H + (hok ? h : 0)) * a.W;
+#pragma unroll
+            for (int j = 0; j < IC; ++j) {
+                const int ww = w0 + j;
+                xv[c][r][j] = (hok && ww >= 0 && ww < a.W) ? row[ww] : 0.0f;
+            }
+        }
+    }
+    const bool ep = epi != 0;
+#pragma unroll 1
+    for (int kk = 0; kk < 16; kk += 4) {
+        float acc[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[u][e] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + kk + u;
+            const int kc = k < a.K ? k : 0;  // wave-uniform
+#pragma unroll
+            for (int c = 0; c < CMAX; ++c) {
+                if (c >= a.C) break;
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int s = 0; s < 3; ++s) {
+                        const float wt = w[((kc * a.C + c) * 3 + r) * 3 + s];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc[u][e] = fmaf(xv[c][r][e * SH + s], wt, acc[u][e]);
+                    }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + kk + u;
+            if (k < a.K) f32s_store4(a, y, n, k, p, q0, acc[u], bias, ep);
+        }
+    }
+}
+
+// Pointwise 1x1 fp32 GEMM on v_mfma_f32_16x16x4_f32: wave = 16 pixels x KT tiles of 16
+// output channels; per MFMA a lane holds one x value (pixel l & 15, channel 4 j + (l >> 4)) and
+// one weight (output channel l & 15 of the tile, same channel): exact products, fp32 sums.
+template <int KT>
+__global__ __launch_bounds__(256) void conv_pw_f32(const float* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, float* __restrict__ y, F32sArgs a,
+                                                   int epi) {
+    const int lane = threadIdx.x & 63;
+    const int v = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (v >= a.items) return;  // wave-uniform
+    const int pg = v % a.PG, sl = v / a.PG;
+    const int kt0 = sl * KT;
+    const int nkt = min(KT, a.NT - kt0);
+    const int g = lane >> 4;
+    const int HW = a.P * a.Q;
+    const int64_t m = (int64_t)pg * 16 + (lane & 15);
+    const bool mok = m < a.M;
+    const int n = mok ? (int)(m / HW) : 0, pp = mok ? (int)(m - (int64_t)n * HW) : 0;
+    const float* xb = x + ((int64_t)n * a.C + g) * HW + pp;
+    const float* wb[KT];
+    bool kok[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        const int k = 16 * (kt0 + t) + (lane & 15);
+        kok[t] = t < nkt && k < a.K;
+        wb[t] = w + (int64_t)(kok[t] ? k : 0) * a.C + g;
+    }
+    floatx4 acc[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nj = (a.C + 3) / 4;
+    for (int j0 = 0; j0 < nj; j0 += 4) {
+        float xa[4], wv[4][KT];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = 4 * (j0 + u) + g;
+            const bool cok = c < a.C;
+            xa[u] = (mok && cok) ? xb[(int64_t)4 * (j0 + u) * HW] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < KT; ++t) wv[u][t] = (kok[t] && cok) ? wb[t][4 * (j0 + u)] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (j0 + u >= nj) break;  // wave-uniform
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+                if (t < nkt) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u], wv[u][t], acc[t], 0, 0, 0);
+        }
+    }
+    // epilogue: lane holds D[pixel 4 g + e][channel lane & 15]
+    const int64_t mo = (int64_t)pg * 16 + 4 * g;
+    const bool ep = epi != 0;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        if (t >= nkt) break;
+        const int k = 16 * (kt0 + t) + (lane & 15);
+        if (k >= a.K) continue;
+        const float bk = bias ? bias[k] : 0.0f;
+        const float s = (ep && a.ps) ? a.ps[k] : 1.0f;
+        const float sh = (ep && a.pb) ? a.pb[k] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t me = mo + e;
+            if (me >= a.M) break;
+            const int ne = (int)(me / HW), pe = (int)(me - (int64_t)ne * HW);
+            const int64_t off = ((int64_t)ne * a.K + k) * HW + pe;
+            float u = acc[t][e] + bk;
+            if (ep) {
+                u = u * s + sh;
+                if (a.res) u += a.res[off];
+                u = epi_act(u, a.act);
+            }
+            y[off] = u;
+        }
+    }
+}
+
+// ---- planning: kinds KIND_DIRECT_F32 (vrx = SH, NJ = CMAX) and KIND_PW_F32 (NJ = KT); the
+// weight is read as given (mode none: no pack, nothing in the workspace)
+void f32s_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
+    out.clear();
+    if (base.groups != 1 || base.dh != 1 || base.dw != 1) return;
+    if ((int64_t)base.N * base.C * base.H * base.W >= (1LL << 31) ||
+        (int64_t)base.N * base.K * base.P * base.Q >= (1LL << 31))
+        return;
+    auto common = [](ConvPlan& p) {
+        p.MI = 0; p.NT = 0; p.TP = p.TQ = 1; p.tilesP = p.tilesQ = 1;
+        p.CC = 0; p.nchunks = 1; p.kblocks = 1; p.HH = p.WW = p.WWp = p.PS = 0;
+        p.steps = 0; p.SB = p.plane = 0; p.taps = p.R * p.S; p.pd = 0; p.nts = 0; p.fp = 0;
+        p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = p.dma_ov = 0;
+        p.packed_floats = 0; p.lds_bytes = 0;
+    };
+    if (base.C <= 4 && base.R == 3 && base.S == 3 && base.sh == base.sw && (base.sh == 1 || base.sh == 2) &&
+        base.ph <= 2 && base.pw <= 2 && base.K <= 1024) {
+        ConvPlan p = base;
+        common(p);
+        p.kind = KIND_DIRECT_F32;
+        p.vrx = base.sh;
+        p.NJ = base.C <= 3 ? 3 : 4;
+        const int64_t items = (int64_t)base.N * base.P * ((base.Q + 3) / 4);
+        p.blocks = (items + 255) / 256;
+        PlanCand c;
+        c.plan = p;
+        c.cost = 0.0;
+        out.push_back(c);
+    }
+    if (base.R == 1 && base.S == 1 && base.sh == 1 && base.sw == 1 && base.ph == 0 && base.pw == 0) {
+        const int NT = (base.K + 15) / 16;
+        const int64_t M = (int64_t)base.N * base.P * base.Q, PG = (M + 15) / 16;
+        for (int kt : {4, 8, 2}) {
+            ConvPlan p = base;
+            common(p);
+            p.kind = KIND_PW_F32;
+            p.vrx = 0;
+            p.NJ = kt;
+            p.NT = NT;
+            const int64_t items = PG * ((NT + kt - 1) / kt);
+            if (items > (int64_t)INT32_MAX - 4) continue;
+            p.blocks = (items + 3) / 4;
+            PlanCand c;
+            c.plan = p;
+            c.cost = 1.0 + kt;
+            out.push_back(c);
+        }
+    }
+}
+
+hipError_t launch_conv_f32s(const ConvPlan& p, const float* x, const float* w, const float* bias, float* y,
+                            const float* ps, const float* pb, const float* res, int act, hipStream_t s) {
+    F32sArgs a;
+    a.N = p.N; a.C = p.C; a.H = p.H; a.W = p.W; a.K = p.K; a.P = p.P; a.Q = p.Q; a.ph = p.ph; a.pw = p.pw;
+    a.ps = ps; a.pb = pb; a.res = res; a.act = act;
+    a.M = (int64_t)p.N * p.P * p.Q;
+    const int epi = (ps || pb || res || act != 0) ? 1 : 0;
+    if (p.kind == KIND_DIRECT_F32) {
+        a.Q4 = (p.Q + 3) / 4;
+        a.items = p.N * p.P * a.Q4;
+        a.KB = 16;
+        const dim3 grid((unsigned)((a.items + 255) / 256), (unsigned)((p.K + 15) / 16)), block(256);
+        if (p.vrx == 1 && p.NJ == 3)
+            hipLaunchKernelGGL((conv_direct_f32<1, 3>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else if (p.vrx == 1)
+            hipLaunchKernelGGL((conv_direct_f32<1, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else if (p.NJ == 3)
+            hipLaunchKernelGGL((conv_direct_f32<2, 3>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else
+            hipLaunchKernelGGL((conv_direct_f32<2, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+        return hipGetLastError();
+    }
+    if (p.kind == KIND_PW_F32) {
+        a.NT = (p.K + 15) / 16;
+        a.PG = (int)((a.M + 15) / 16);
+        a.items = a.PG * ((a.NT + p.NJ - 1) / p.NJ);
+        const dim3 grid((unsigned)((a.items + 3) / 4)), block(256);
+        switch (p.NJ) {
+            case 2: hipLaunchKernelGGL((conv_pw_f32<2>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 4: hipLaunchKernelGGL((conv_pw_f32<4>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 8: hipLaunchKernelGGL((conv_pw_f32<8>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace po2q

@@ -27,7 +27,21 @@ hipError_t launch_quantize_plain(const float* w, int64_t n, const unsigned* part
                                  int bits, int fsr, int mode, float* out, hipStream_t s);
 
 // Conv kinds
-enum ConvKind { KIND_MFMA_F32 = 0, KIND_DEPTHWISE = 1, KIND_BF16X3 = 2, KIND_BF16X3_DMA = 3, KIND_BF16X3_ROWS = 4 };
+enum ConvKind {
+    KIND_MFMA_F32 = 0,
+    KIND_DEPTHWISE = 1,
+    KIND_BF16X3 = 2,
+    KIND_BF16X3_DMA = 3,
+    KIND_BF16X3_ROWS = 4,
+    KIND_BF16X3_PW = 5,  // 1x1 / stride 1 GEMM kernel (po2q_conv_pw.hip)
+    KIND_DIRECT_F32 = 6,  // unquantized 3-channel stems, direct fp32 (po2q_conv_f32s.hip)
+    KIND_PW_F32 = 7       // unquantized 1x1 convs, fp32 MFMA GEMM (po2q_conv_f32s.hip)
+};
+
+// Every kind whose weight is packed as exact bf16 +-2^e fragments + one fp32 scale.
+inline bool is_bf16x3_kind(int kind) {
+    return kind == KIND_BF16X3 || kind == KIND_BF16X3_DMA || kind == KIND_BF16X3_ROWS || kind == KIND_BF16X3_PW;
+}
 
 // Conv geometry and tiling plan (host-side, shared by workspace sizing and launch).
 struct ConvPlan {
@@ -106,6 +120,19 @@ bool plan_bf16x3_dma(ConvPlan& p);
 // Row-streaming bf16x3 candidates (po2q_conv_rows.hip: 3x3 / stride 1 / C in {16, 32});
 // empty if not eligible.
 void rows_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+
+// Pointwise 1x1 / stride-1 candidates (po2q_conv_pw.hip), cost-ranked; empty if not eligible.
+void pw_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+// Its launch, the eval epilogue (ps / pb / res may be NULL, act PO2Q_ACT_*) in the store.
+hipError_t launch_conv_pw(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                          const float* bias, float* y, const float* ps, const float* pb, const float* res, int act,
+                          hipStream_t s);
+
+// fp32 kernels for mode none (po2q_conv_f32s.hip): candidates (empty if not eligible) and the
+// launch with the eval epilogue in the store; the weight is read as given (no pack).
+void f32s_candidates(const ConvPlan& base, std::vector<PlanCand>& out);
+hipError_t launch_conv_f32s(const ConvPlan& p, const float* x, const float* w, const float* bias, float* y,
+                            const float* ps, const float* pb, const float* res, int act, hipStream_t s);
 
 // Pack (and quantize unless mode == 0) the weight into the plan's layout.
 hipError_t launch_pack_weights(const ConvPlan& p, const float* w, const unsigned* partial, int nparts,

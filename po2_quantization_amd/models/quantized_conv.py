@@ -107,14 +107,33 @@ def act_name(m):
     return _ACT_NAMES.get(type(m))
 
 
+def _fold_key(bn):
+    ts = [bn.running_var, bn.running_mean] + ([bn.weight, bn.bias] if bn.affine else [])
+    return (bn.eps,) + tuple((t.data_ptr(), t._version, t.device) for t in ts)
+
+
 def fold_bn(bn):
     """Eval BatchNorm as (post_scale, post_shift): y = x * s + t (torch batch_norm in eval:
-    (x - mean) / sqrt(var + eps) * weight + bias)."""
-    s = torch.rsqrt(bn.running_var + bn.eps)
-    if bn.affine:
-        s = s * bn.weight
-        return s, bn.bias - bn.running_mean * s
-    return s, -bn.running_mean * s
+    (x - mean) / sqrt(var + eps) * weight + bias).
+
+    Cached on the module, keyed on the storage and version counter of its statistics and
+    affine parameters (any in-place update, load_state_dict or .to() changes the key): an eval
+    forward then issues no elementwise launches for its BatchNorms (five small kernels per
+    conv otherwise -- the host-side cost that made the eager fused MobileViT forward slower than
+    the unfused one)."""
+    key = _fold_key(bn)
+    hit = getattr(bn, "_po2q_fold", None)
+    if hit is not None and hit[0] == key:
+        return hit[1], hit[2]
+    with torch.no_grad():
+        s = torch.rsqrt(bn.running_var + bn.eps)
+        if bn.affine:
+            s = s * bn.weight
+            t = bn.bias - bn.running_mean * s
+        else:
+            t = -bn.running_mean * s
+    bn._po2q_fold = (key, s, t)
+    return s, t
 
 
 # Inference fusion switch (tools/model_bench.py times both sides).
@@ -215,13 +234,30 @@ class QuantizedConv2d(nn.Conv2d):
 
 
 
+def plain_conv_fused(conv, x, bn=None, act=None, residual=None):
+    """An unquantized nn.Conv2d (the reference's stems and last 1x1 convs: resnet.py:99-102,
+    mobilenet.py:41-50, mobile_vit.py:41-48) with the eval BatchNorm / activation after it, as
+    ONE native call of the fp32 path (mode "none": exact fp32 products, fp32 accumulation)."""
+    if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
+        raise RuntimeError("po2q: fused plain conv needs numeric zero padding")
+    ps, pb = fold_bn(bn) if bn is not None else (None, None)
+    return _lib.qconv2d_fused(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, 4,
+                              "none", 1, "auto", post_scale=ps, post_shift=pb, residual=residual, act=act or "none")
+
+
+def _native_ok(x):
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+
+
 def fusable_sequence(seq):
-    """True when seq is (QuantizedConv2d, BatchNorm[, activation])* -- the conv blocks of
-    the reference's models (mobilenet.py:53-131, mobile_vit.py:15-39, 131-233)."""
+    """True when seq is (conv, BatchNorm[, activation])* -- the conv blocks of the reference's
+    models (mobilenet.py:53-131, mobile_vit.py:15-48, 131-233); conv is a QuantizedConv2d or an
+    unquantized nn.Conv2d with numeric zero padding."""
     mods = list(seq)
     i = 0
     while i < len(mods):
-        if not isinstance(mods[i], QuantizedConv2d):
+        c = mods[i]
+        if not isinstance(c, nn.Conv2d) or c.padding_mode != "zeros" or isinstance(c.padding, str):
             return False
         i += 1
         if i < len(mods) and isinstance(mods[i], nn.modules.batchnorm._BatchNorm):
@@ -248,5 +284,17 @@ def run_fused_sequence(seq, x, residual=None):
         act = act_name(mods[i]) if i < len(mods) else None
         if act is not None:
             i += 1
-        x = conv.fused(x, bn=bn, act=act, residual=residual if i >= len(mods) else None)
+        res = residual if i >= len(mods) else None
+        if isinstance(conv, QuantizedConv2d):
+            x = conv.fused(x, bn=bn, act=act, residual=res)
+        else:
+            x = plain_conv_fused(conv, x, bn=bn, act=act, residual=res)
     return x
+
+
+def run_sequence(seq, x):
+    """seq(x): the fused native calls in eval (can_fuse) when seq is a fusable conv block and x a
+    HIP fp32 tensor, else the module sequence itself."""
+    if _native_ok(x) and can_fuse(*seq) and fusable_sequence(seq):
+        return run_fused_sequence(seq, x)
+    return seq(x)

@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..utils.quantizers import NATIVE_MODES
-from .quantized_conv import QuantizedConv2d, can_fuse, fold_bn, run_fused_sequence
+from .quantized_conv import QuantizedConv2d, can_fuse, fold_bn, plain_conv_fused, run_fused_sequence
 
 
 class BasicBlock(nn.Module):
@@ -143,7 +143,11 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.relu(self.bn1(self.conv1(x)))
+        if can_fuse(self.bn1) and x.is_cuda and x.dtype == torch.float32:
+            # the unquantized stem conv + bn1 + relu (resnet.py:99-102, 191) as one native fp32 call
+            x = plain_conv_fused(self.conv1, x, bn=self.bn1, act="relu")
+        else:
+            x = self.relu(self.bn1(self.conv1(x)))
         x = self.layer3(self.layer2(self.layer1(x)))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -419,3 +419,89 @@ def test_nonfinite_inputs_pair_and_s2ds(C, W):
     y3, yd = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2")
     assert _same_nonfinite(y3.cpu(), _oracle_ref(x, w3, 2, 1))
     assert _same_nonfinite(yd.cpu(), _oracle_ref(x, wd, 2, 0))
+
+
+PW_SHAPES = [  # N, C, HW side, K: MobileNetV2 @32 expand / project convs and odd edges
+    (4, 16, 16, 96), (4, 96, 8, 24), (3, 24, 8, 144), (4, 144, 4, 32), (5, 160, 2, 960), (5, 960, 2, 160),
+    (3, 32, 7, 64),   # HW = 49: 16-pixel groups span images, scalar stores
+    (2, 8, 3, 12),    # C < 32, K < 16
+    (7, 320, 1, 40),  # HW = 1
+]
+
+
+@pytest.mark.parametrize("shape", PW_SHAPES, ids=[str(s) for s in PW_SHAPES])
+@pytest.mark.parametrize("mode", ["po2", "po2+"])
+def test_pointwise_kernel_every_plan_vs_oracle(shape, mode):
+    """The 1x1 GEMM kernel (kind bf16x3_pw: MobileNetV2 / MobileViT pointwise convs, reference
+    models/mobilenet.py:78-93,120) is the planned kernel for every 1x1 / stride-1 shape, and every
+    candidate plan meets the bar against the oracle, plain and with the fused BN + ReLU6 +
+    residual epilogue (mobilenet.py:120-134)."""
+    N, C, Hs, K = shape
+    g = torch.Generator().manual_seed(N + C + K)
+    x = torch.randn(N, C, Hs, Hs, generator=g)
+    w = torch.randn(K, C, 1, 1, generator=g) * 0.2
+    ps, pb = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1
+    res = torch.randn(N, K, Hs, Hs, generator=g)
+    ref, _ = O.qconv2d(x.numpy(), w.numpy(), None, 1, 0, 1, 1, 4, mode)
+    ref_e = np.clip(ref * ps.numpy().astype(np.float64).reshape(1, -1, 1, 1) +
+                    pb.numpy().astype(np.float64).reshape(1, -1, 1, 1) + res.numpy().astype(np.float64), 0.0, 6.0)
+    assert "kind=bf16x3_pw" in _lib.describe(N, C, Hs, Hs, K, 1, 1, 1, 0, 1, 1, 4, mode)
+    xd, wd = x.to(DEV), w.to(DEV)
+    plans = _lib.plans(N, C, Hs, Hs, K, 1, 1, 1, 0, 1, 1, 4, mode)
+    assert sum("kind=bf16x3_pw" in d for d in plans) >= 1
+    for i, desc in enumerate(plans):
+        y = _lib.qconv2d(xd, wd, None, 1, 0, 1, 1, 4, mode, plan=i).cpu().numpy()
+        assert normwise_err(y, ref) <= CONV_TOL, (desc, normwise_err(y, ref))
+    y = _lib.qconv2d_fused(xd, wd, None, 1, 0, 1, 1, 4, mode, post_scale=ps.to(DEV), post_shift=pb.to(DEV),
+                           residual=res.to(DEV), act="relu6").cpu().numpy()
+    assert normwise_err(y, ref_e) <= CONV_TOL, normwise_err(y, ref_e)
+
+
+def test_plain_conv_fused_stem_vs_torch():
+    """The unquantized stems (resnet.py:99-102, mobilenet.py:41-46) as one native fp32 call with
+    their eval BN + activation, against torch's fp32 module sequence."""
+    from po2_quantization_amd.models.quantized_conv import plain_conv_fused
+
+    torch.manual_seed(0)
+    for cin, cout, k, st, act, mod in ((3, 16, 3, 1, "relu", torch.nn.ReLU()), (3, 32, 3, 2, "relu6", torch.nn.ReLU6()),
+                                       (320, 1280, 1, 1, "relu6", torch.nn.ReLU6())):
+        conv = torch.nn.Conv2d(cin, cout, k, st, k // 2, bias=False).to(DEV)
+        bn = torch.nn.BatchNorm2d(cout).to(DEV).eval()
+        with torch.no_grad():
+            bn.running_mean.normal_(0, 0.1)
+            bn.running_var.uniform_(0.5, 1.5)
+            x = torch.randn(4, cin, 32 if k == 3 else 4, 32 if k == 3 else 4, device=DEV)
+            y = plain_conv_fused(conv, x, bn=bn, act=act)
+            ref = mod(bn(conv(x)))
+        assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL
+
+
+F32S_SHAPES = [  # N, C, H, W, K, R, stride, pad: unquantized stems and 1x1 convs (mode none)
+    (2, 3, 32, 32, 16, 3, 1, 1), (2, 3, 33, 30, 32, 3, 2, 1), (3, 3, 15, 13, 16, 3, 2, 1), (2, 1, 9, 7, 20, 3, 1, 1),
+    (2, 4, 10, 12, 24, 3, 1, 1), (4, 320, 2, 2, 1280, 1, 1, 0), (3, 96, 5, 5, 384, 1, 1, 0), (2, 30, 7, 7, 50, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("shape", F32S_SHAPES, ids=[str(s) for s in F32S_SHAPES])
+def test_unquantized_kernels_every_plan_vs_oracle(shape):
+    """Mode "none" (the reference's plain nn.Conv2d stems / last 1x1 conv, and lin / lin+ weights):
+    the direct fp32 stem kernel and the fp32-MFMA pointwise kernel, every candidate plan, plain and
+    with the fused BN + ReLU6 epilogue, against the oracle's fp64 conv."""
+    N, C, H, W, K, R, st, pad = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, R, R, generator=g) * 0.3
+    b = torch.randn(K, generator=g) * 0.1
+    ps, pb = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1
+    ref, _ = O.qconv2d(x.numpy(), w.numpy(), b.numpy(), st, pad, 1, 1, 4, "none")
+    ref_e = np.clip(ref * ps.numpy().astype(np.float64).reshape(1, -1, 1, 1) +
+                    pb.numpy().astype(np.float64).reshape(1, -1, 1, 1), 0.0, 6.0)
+    desc0 = _lib.describe(N, C, H, W, K, R, R, st, pad, 1, 1, 4, "none")
+    assert ("kind=direct_f32" in desc0) if R == 3 else ("kind=pw_f32" in desc0), desc0
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    for i, desc in enumerate(_lib.plans(N, C, H, W, K, R, R, st, pad, 1, 1, 4, "none")):
+        y = _lib.qconv2d(xd, wd, bd, st, pad, 1, 1, 4, "none", plan=i).cpu().numpy()
+        assert normwise_err(y, ref) <= CONV_TOL, (desc, normwise_err(y, ref))
+    y = _lib.qconv2d_fused(xd, wd, bd, st, pad, 1, 1, 4, "none", post_scale=ps.to(DEV), post_shift=pb.to(DEV),
+                           act="relu6").cpu().numpy()
+    assert normwise_err(y, ref_e) <= CONV_TOL

@@ -44,6 +44,8 @@ for s in $STEPS; do
                 run models_c4 300 python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
         profmb) run profmb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profmb -o run \
                   -- python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --only-fused ;;
+        profr56) run profr56 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profr56 -o run \
+                  -- python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
         bwdtests) run bwdtests 600 python -u -m pytest tests/test_gpu_backward.py tests/test_qat.py -m gpu -x -q --timeout 300 --timeout-method thread
                if ! grep -q " passed" gpurun_out/bwdtests.log || grep -q "failed\|error" gpurun_out/bwdtests.log; then
                    echo "stopping: backward GPU tests did not pass"; exit 1
@@ -60,6 +62,10 @@ for s in $STEPS; do
         pairstg) run pairstg 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123,10023,23 python tools/pair_bench.py ;;
         pairablate) run pairablate 300 python tools/pair_ablate.py ;;
         pairpd) run pairpd 300 env PAIR_C32=0 PAIR_VARIANTS=23,33,43,123,133,143 python tools/pair_bench.py ;;
+        abc32) for r in 1 2; do
+                   run abc32_off_$r 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
+                   run abc32_on_$r 300 env PO2Q_PAIR_C32=1 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
+               done ;;
         pairq) run pairq 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123 python tools/pair_bench.py ;;
         benchq) run benchq 300 python bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-cifar ;;
         abstg) for r in 1 2; do for v in 123 10123 10023; do
