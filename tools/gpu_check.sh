@@ -67,7 +67,7 @@ for s in $STEPS; do
                    run abc32_on_$r 300 env PO2Q_PAIR_C32=1 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
                done ;;
         pairq) run pairq 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123 python tools/pair_bench.py ;;
-        benchq) run benchq 300 python bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-cifar ;;
+        benchq) run benchq 300 python bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-cifar --no-models ;;
         abstg) for r in 1 2; do for v in 123 10123 10023; do
                    run abstg_${v}_$r 300 env PO2Q_PAIR_VARIANT=$v python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
                done; done ;;
@@ -124,7 +124,7 @@ for s in $STEPS; do
         ablate1) run ablate1 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so python tools/ablate.py --shape 16,224,16,3,1,1 --plans 2,3 ;;
         ablate) run ablate 600 env PO2Q_LIB=$PWD/po2_quantization_amd/lib_stamps/libpo2q.so bash -c 'python tools/ablate.py --shape 16,224,16,3,1,1 && python tools/ablate.py --shape 32,112,32,3,1,1 && python tools/ablate.py --shape 64,56,64,3,1,1' ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-                  -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cifar ;;
+                  -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cifar --no-models ;;
         *) echo "unknown step $s" ;;
     esac
 done
