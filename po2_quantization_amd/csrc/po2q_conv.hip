@@ -363,7 +363,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             if (!dup) out.push_back(c);
         }
     };
-    add(pwc, 3);
+    add(pwc, 8);
     add(rows, kTuneRowsCands);
     add(reg, kTuneRegCands);
     add(dma, kTuneDmaCands);

@@ -39,13 +39,19 @@ struct PwArgs {
     int act;
 };
 
-template <int KT, bool EPI>
+// KSPLIT 1: a block = 4 independent wave items.  KSPLIT 4 (few items: late MobileNetV2 layers
+// at 2x2 / 1x1 pixels, where 16-pixel groups are few and C is up to 960): a block = ONE item,
+// wave w takes the k-steps ks = w mod 4, and the 4 partial sums are added through LDS in a
+// fixed order (deterministic) before wave 0's epilogue -- a 4x shorter dependent load chain.
+template <int KT, bool EPI, int KSPLIT = 1>
 __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, const uint4* __restrict__ wp,
                                                const float* __restrict__ scale_p, const float* __restrict__ bias,
                                                float* __restrict__ y, PwArgs a) {
     const int lane = threadIdx.x & 63;
-    const int v = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (v >= a.items) return;  // wave-uniform (no block-wide synchronisation in this kernel)
+    const int wv = (int)(threadIdx.x >> 6);
+    const int v = KSPLIT == 1 ? (int)blockIdx.x * 4 + wv : (int)blockIdx.x;
+    if (v >= a.items) return;  // KSPLIT 1: wave-uniform; KSPLIT 4: block-uniform
+    const int ks0 = KSPLIT == 1 ? 0 : wv;
     const int pg = v % a.PG, sl = v / a.PG;
     const int kt0 = sl * KT;
     const int nkt = min(KT, a.NT - kt0);
@@ -69,10 +75,10 @@ __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, cons
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     uint32_t cur[8];
-    load8(0, cur);
-    for (int ks = 0; ks < a.KS; ++ks) {
+    if (ks0 < a.KS) load8(ks0, cur);
+    for (int ks = ks0; ks < a.KS; ks += KSPLIT) {
         uint32_t nxt[8];
-        if (ks + 1 < a.KS) load8(ks + 1, nxt);
+        if (ks + KSPLIT < a.KS) load8(ks + KSPLIT, nxt);
         uint4 bw[KT];
 #pragma unroll
         for (int t = 0; t < KT; ++t)
@@ -90,10 +96,23 @@ __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, cons
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, acc[t], 0, 0, 0);
             }
         }
-        if (ks + 1 < a.KS) {
+        if (ks + KSPLIT < a.KS) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) cur[e] = nxt[e];
         }
+    }
+    if constexpr (KSPLIT > 1) {
+        __shared__ floatx4 part[KSPLIT - 1][KT][64];
+        if (wv > 0) {
+#pragma unroll
+            for (int t = 0; t < KT; ++t) part[wv - 1][t][lane] = acc[t];
+        }
+        __syncthreads();
+        if (wv > 0) return;
+#pragma unroll
+        for (int w = 0; w < KSPLIT - 1; ++w)
+#pragma unroll
+            for (int t = 0; t < KT; ++t) acc[t] += part[w][t][lane];
     }
 
     // epilogue: lane holds D[pixel 4 g + e][channel lane & 15] of each tile
@@ -147,7 +166,7 @@ __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, cons
 
 // Plan: kind KIND_BF16X3_PW, packed weight in the generic bf16x3 layout with one chunk of
 // CC = C rounded up to 32 channels (pack_bf16x3_kernel: [ks][nt][lane][8]), NJ = KT.
-static bool pw_plan_one(ConvPlan& p, int kt) {
+static bool pw_plan_one(ConvPlan& p, int kt, int ksplit) {
     const int NT = (p.K + 15) / 16, KS = (p.C + 31) / 32;
     p.kind = KIND_BF16X3_PW;
     p.vrx = 0;
@@ -163,7 +182,7 @@ static bool pw_plan_one(ConvPlan& p, int kt) {
     p.tilesP = p.tilesQ = 1;
     p.HH = p.WW = p.WWp = p.PS = 0;
     p.SB = p.plane = 0;
-    p.pd = 0;
+    p.pd = ksplit;  // k-steps split over the block's 4 waves (1: none)
     p.nts = 0;
     p.fp = 0;
     p.dma_d0 = p.dma_nck = p.dma_ni = p.dma_nw = p.dma_waves = p.dma_ov = 0;
@@ -173,7 +192,7 @@ static bool pw_plan_one(ConvPlan& p, int kt) {
     const int64_t PG = (M + 15) / 16;
     const int64_t items = PG * ((NT + kt - 1) / kt);
     if (items > (int64_t)INT32_MAX - 4 || PG > INT32_MAX) return false;
-    p.blocks = (items + 3) / 4;
+    p.blocks = ksplit == 1 ? (items + 3) / 4 : items;
     return true;
 }
 
@@ -191,19 +210,22 @@ void pw_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
     const int NT = (base.K + 15) / 16;
     const int64_t M = (int64_t)base.N * base.P * base.Q;
     const int64_t PG = (M + 15) / 16;
-    for (int kt : {2, 4, 8}) {
-        if (kt > 2 && (NT + kt / 2 - 1) / (kt / 2) <= 1) continue;  // no wider than the channel count needs
-        ConvPlan p = base;
-        if (!pw_plan_one(p, kt)) continue;
-        // cost: waves of work, penalising too few waves to fill the chip (< 4 per CU)
-        const int64_t waves = PG * ((NT + kt - 1) / kt);
-        const double fill = std::min(1.0, (double)waves / 4096.0);
-        const double per_wave = 40.0 + 3.0 * std::min(kt, NT) * ((base.C + 31) / 32) * 16.0 / 8.0 +
-                                ((base.C + 31) / 32) * 24.0;
-        PlanCand c;
-        c.plan = p;
-        c.cost = waves * per_wave / fill;
-        out.push_back(c);
+    const int KS = (base.C + 31) / 32;
+    for (int ksplit : {1, 4}) {
+        for (int kt : {2, 4, 8}) {
+            if (kt > 2 && (NT + kt / 2 - 1) / (kt / 2) <= 1) continue;  // no wider than the channel count needs
+            if (ksplit > 1 && KS < 2 * ksplit) continue;                 // too few k-steps to split
+            ConvPlan p = base;
+            if (!pw_plan_one(p, kt, ksplit)) continue;
+            // cost: the dependent k-step chain of a wave, scaled up when too few waves fill the chip
+            const int64_t waves = PG * ((NT + kt - 1) / kt) * ksplit;
+            const double fill = std::min(1.0, (double)waves / 4096.0);
+            const double chain = ((KS + ksplit - 1) / ksplit) * (24.0 + 3.0 * 16.0 * std::min(kt, NT) / 8.0) + 40.0;
+            PlanCand c;
+            c.plan = p;
+            c.cost = (double)waves * chain / ksplit / fill + (fill < 1.0 ? chain * 64.0 : 0.0);
+            out.push_back(c);
+        }
     }
     std::stable_sort(out.begin(), out.end(), [](const PlanCand& u, const PlanCand& v) { return u.cost < v.cost; });
 }
@@ -212,10 +234,16 @@ template <int KT>
 static hipError_t launch_pw_t(const ConvPlan& p, const PwArgs& a, const float* x, const uint4* wp, const float* scale,
                               const float* bias, float* y, bool epi, hipStream_t s) {
     const dim3 grid((unsigned)p.blocks), block(256);
-    if (epi)
+    if (p.pd == 4) {
+        if (epi)
+            hipLaunchKernelGGL((conv_pw<KT, true, 4>), grid, block, 0, s, x, wp, scale, bias, y, a);
+        else
+            hipLaunchKernelGGL((conv_pw<KT, false, 4>), grid, block, 0, s, x, wp, scale, bias, y, a);
+    } else if (epi) {
         hipLaunchKernelGGL((conv_pw<KT, true>), grid, block, 0, s, x, wp, scale, bias, y, a);
-    else
+    } else {
         hipLaunchKernelGGL((conv_pw<KT, false>), grid, block, 0, s, x, wp, scale, bias, y, a);
+    }
     return hipGetLastError();
 }
 

@@ -426,6 +426,7 @@ PW_SHAPES = [  # N, C, HW side, K: MobileNetV2 @32 expand / project convs and od
     (3, 32, 7, 64),   # HW = 49: 16-pixel groups span images, scalar stores
     (2, 8, 3, 12),    # C < 32, K < 16
     (7, 320, 1, 40),  # HW = 1
+    (4, 960, 1, 160),  # HW = 1, C = 960: the split-K candidates
 ]
 
 
