@@ -545,6 +545,334 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
 }
 
+
+// ------------------------------------------------------------- role-split pair --
+// conv_pair_ab: the same C = 16 BasicBlock chain as conv_pair with the two convs given to
+// different waves.  8 waves (W <= 256: 2 x ceil(W / 64)): waves 0 .. NR-1 ("A") own 64 output
+// columns each of conv 1 -- x DMA, exact split, 72 transposed MFMAs per step, and the epilogue-1
+// split of the intermediate row into the shared planes; waves NR .. 2 NR - 1 ("B") own the same
+// columns of conv 2 -- 72 MFMAs on the shared planes, epilogue 2, the output stores.  A block's
+// waves go to the SIMDs in a cyclic order, so wave w and wave w + 4 share a SIMD: each SIMD pairs
+// an A wave with a B wave.  Why: in conv_pair every wave runs conv 2 then conv 1 behind one
+// barrier, so the two waves of a SIMD issue their MFMAs, then their VALU splits, at the same
+// time (tools/pair_ablate.py: compute alone 0.39 ms, memory alone 0.36 ms, together 0.56 ms).
+// Here A opens each step with VALU (the deferred epilogue 1 of the row completed one step
+// earlier, then the split of x) while B opens with MFMAs, and A's MFMAs run beside B's epilogue
+// and stores.  Deferring epilogue 1 by one step makes B lag conv_pair's conv 2 by one row:
+// step j: A splits x row j, conv 1 -> intermediate row j - 2 completes (epilogue at step j + 1);
+//         B: conv 2 on intermediate row j - 4 (written at step j - 1), output row j - 6.
+// Arithmetic identical to conv_pair (same splits, same MFMA order per accumulator).
+constexpr int kABSW = 64;                        // output columns per wave (4 x 16-pixel groups)
+constexpr int kABPlane = (kABSW + 2) * 32 + 32;  // a wave's x planes: [66 px][16 ch] bf16 + zero slot
+
+struct PairABArgs {
+    int N, H, W;
+    int Wp;   // 64 x NR
+    int YPL;  // bytes of one shared intermediate plane: (Wp + 3) px x 32 B
+    int RB, nseg, items, remap;
+    int NR;   // waves per role
+    WQuant q1, q2;
+    const float* b1;
+    const float* b2;
+    const float* ps1;
+    const float* pb1;
+    const float* ps2;
+    const float* pb2;
+    int act1, act2;
+};
+
+template <int E>
+__global__ __launch_bounds__(512, 1) void conv_pair_ab(const float* __restrict__ x, float* __restrict__ y,
+                                                       PairABArgs a) {
+    constexpr int CC = 16, SW = kABSW, WC = SW + 2, PL = kABPlane, KS = 2, NG = SW / 16, NF = 3 * KS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nw = (int)(blockDim.x >> 6);
+    const int NR = a.NR;
+    const bool isA = wave < NR;  // wave-uniform
+    const int wr = isA ? wave : wave - NR;
+    const int rawslot = CC * a.Wp * 4;
+    const int yslot = 3 * a.YPL;
+    unsigned char* raw = lds;                                 // 2 x [16][Wp] fp32 (x rows)
+    unsigned char* yr = raw + 2 * rawslot;                    // 2 x 3 planes (intermediate)
+    unsigned char* slab = yr + 2 * yslot + wr * (3 * PL);     // A: this wave's x planes
+    const int zero_off = WC * CC * 2;
+    const int yzero = (a.Wp + 2) * (2 * CC);
+
+    int blk = blockIdx.x;
+    if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
+    if (blk >= a.items) return;  // block-uniform
+    const int seg = blk % a.nseg;
+    const int n = blk / a.nseg;
+    const int p0 = seg * a.RB;
+    const int rbe = min(a.RB, a.H - p0);
+    const int nx = rbe + 4;      // x rows p0-2 .. p0+rbe+1
+    const int n1 = rbe + 2;      // intermediate rows p0-1 .. p0+rbe
+    const int nsteps = nx + 2;   // output row p0 + o completes at step o + 6
+    const int q0 = wr * SW;
+    const int HW = a.H * a.W;
+
+    // ---- A: x DMA, 4 instructions per wave: lane l of instruction i -> float4 e = 64 (4 wr + i) + l
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
+    const int W4 = a.Wp >> 2;
+    uint32_t vi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = 64 * (4 * wr + i) + lane;
+        const int c = e / W4, q = 4 * (e - c * W4);
+        vi[i] = (isA && q < a.W) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
+    }
+    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    auto load_row = [&](int sl, int jn) __attribute__((always_inline)) {
+        const int h = p0 - 2 + jn;
+        const bool hok = jn < nx && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(4 * wr) * 1024u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            rows_dma16<true>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
+    };
+
+    // ---- A: split lanes: column sc = lane of the strip, both channel octets; halo lanes < 32
+    const int hside = lane >> 4, hch = lane & 15;
+    const int hq = hside ? q0 + SW : q0 - 1;
+    const bool h_ok = lane < 2 * CC && hq >= 0 && hq < a.W;
+    const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
+    const int rdx0 = (q0 + lane) * 4;
+    const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
+    int aoff[NG][KS], yoff[NG][KS];
+    {
+        const int p = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            const int qc = q0 + 16 * grp + p;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int sh = ks == 0 ? (g >> 1) : 2;
+                const bool zero = ks == 1 && g >= 2;
+                aoff[grp][ks] = zero ? zero_off : xa<CC>(16 * grp + p + sh, g & 1);
+                yoff[grp][ks] = zero ? yzero : yoct<CC>(qc + sh, g & 1);
+            }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * CC * HW, CC * HW * 4);
+
+    float scale1 = 1.0f, scale2 = 1.0f;
+    bool fin1 = true, fin2 = true;
+    bf16x8 bw[NF];  // A: conv 1's fragments (transposed form), B: conv 2's
+    float ek1[E ? 4 : 1], ek0[E ? 4 : 1];   // A: epilogue 1 folded: t = act1(acc * ek1[c] + ek0[c]), c = 4 (lane >> 4) + e
+    float ek2s = 1.0f, ek2b = 0.0f;         // B: channel lane & 15: v = acc * ek2s + ek2b
+    floatx4 acc[3][NG];
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) acc[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // 3 tap rows x 2 k-steps x 3 planes x 4 groups of MFMAs on one split row into slots SL of S
+    auto mfmas = [&](auto S_, auto TR_, const unsigned char* pb, int plstride) __attribute__((always_inline)) {
+        constexpr int S = decltype(S_)::value;
+        constexpr bool TR = decltype(TR_)::value;
+        constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 af[3][NG];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int grp = 0; grp < NG; ++grp)
+                    af[pl][grp] = __builtin_bit_cast(
+                        bf16x8, *reinterpret_cast<const uint4*>(pb + pl * plstride + (TR ? aoff[grp][ks] : yoff[grp][ks])));
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const bf16x8 b = bw[rr * KS + ks];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int grp = 0; grp < NG; ++grp)
+                        acc[SL[rr]][grp] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], acc[SL[rr]][grp], 0, 0, 0)
+                                              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, acc[SL[rr]][grp], 0, 0, 0);
+            }
+        }
+    };
+
+    // A: epilogue 1 of intermediate row i from slot D (values split straight into ring slot YW)
+    auto epi1 = [&](auto D_, auto YW_, int i) __attribute__((always_inline)) {
+        constexpr int D = decltype(D_)::value, YW = decltype(YW_)::value;
+        const int r1 = p0 - 1 + i;
+        const bool irow = i >= 0 && i < n1 && r1 >= 0 && r1 < a.H;
+        const int p = lane & 15, g = lane >> 4;
+        unsigned char* yw = yr + YW * yslot;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            const int q = q0 + 16 * grp + p;  // lane: pixel q, channels 4 g .. 4 g + 3
+            const bool ok = irow && q < a.W;
+            uint32_t b4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float t;
+                if constexpr (E == 0)
+                    t = acc[D][grp][e] * scale1 + 0.0f;
+                else
+                    t = epi_act(acc[D][grp][e] * ek1[e] + ek0[e], a.act1);
+                b4[e] = ok ? __float_as_uint(t) : 0u;
+            }
+            uint16_t h[4], m[4], l[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
+            const int wo = yoct<CC>(q + 1, g >> 1) + 8 * (g & 1);
+            *reinterpret_cast<uint2*>(yw + wo) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+            *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
+                make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+            *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
+                make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+            acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    // B: epilogue 2 of output row o from slot D: whole 128-byte lines per store (the DPP
+    // exchange of conv_pair's epi2 on group pairs (0, 1) and (2, 3))
+    auto epi2 = [&](auto D_, int o) __attribute__((always_inline)) {
+        constexpr int D = decltype(D_)::value;
+        const bool orow = o >= 0 && o < rbe;
+        const int g = lane >> 4;
+        const bool hi8 = (lane & 8) != 0;
+#pragma unroll
+        for (int gp = 0; gp < NG / 2; ++gp) {
+            floatx4 v0, v1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float u0 = acc[D][2 * gp][e] * ek2s + ek2b, u1 = acc[D][2 * gp + 1][e] * ek2s + ek2b;
+                if constexpr (E != 0) {
+                    u0 = epi_act(u0, a.act2);
+                    u1 = epi_act(u1, a.act2);
+                }
+                v0[e] = u0;
+                v1[e] = u1;
+            }
+            floatx4 sa, sb;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v1[e]), 0x128, 0xf, 0xf, false));
+                const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v0[e]), 0x128, 0xf, 0xf, false));
+                sa[e] = hi8 ? r1 : v0[e];
+                sb[e] = hi8 ? v1[e] : r0;
+            }
+            const int q = q0 + 32 * gp + (hi8 ? 16 : 0) + 4 * g;
+            const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
+            const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
+            const bool ok = orow && q < a.W;
+            rows_store<true>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+            rows_store<true>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+            acc[D][2 * gp] = floatx4{0.f, 0.f, 0.f, 0.f};
+            acc[D][2 * gp + 1] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    auto step = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S6 = decltype(S_)::value;
+        constexpr int S = S6 % 3;
+        if (isA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x row j (own DMAs)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (isA) {
+            load_row((S6 + 1) & 1, j + 1);  // row j + 1 into the slot of row j - 1
+            const unsigned char* rw = raw + (S6 & 1) * rawslot;
+            uint32_t bx[2][8], hx;
+#pragma unroll
+            for (int so = 0; so < 2; ++so)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    bx[so][e] = *reinterpret_cast<const uint32_t*>(rw + (8 * so + e) * (a.Wp * 4) + rdx0);
+            hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
+            // the deferred epilogue 1: intermediate row j - 3, completed at step j - 1 (slot D of
+            // S6 - 1), into ring slot (j - 3) & 1
+            epi1(std::integral_constant<int, ((S6 + 5) % 3 + 2) % 3>{}, std::integral_constant<int, (S6 + 1) & 1>{},
+                 j - 3);
+#pragma unroll
+            for (int so = 0; so < 2; ++so) {
+                uint4 hi, mid, lo;
+                split3(bx[so], hi, mid, lo);
+                const int wa = xa<CC>(lane + 1, so);
+                *reinterpret_cast<uint4*>(slab + wa) = hi;
+                *reinterpret_cast<uint4*>(slab + PL + wa) = mid;
+                *reinterpret_cast<uint4*>(slab + 2 * PL + wa) = lo;
+            }
+            if (lane < 2 * CC) {
+                uint16_t h16, m16, l16;
+                split1(h_ok ? hx : 0u, h16, m16, l16);
+                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+                *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
+                *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
+            }
+            mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab, PL);
+        } else {
+            // conv 2 one step behind conv_pair's: intermediate row j - 4 from ring slot j & 1,
+            // the rotation of step j - 1, output row j - 6 completes
+            constexpr int SB = (S6 + 5) % 3;
+            if (j >= 4) mfmas(std::integral_constant<int, SB>{}, std::false_type{}, yr + (S6 & 1) * yslot, a.YPL);
+            epi2(std::integral_constant<int, (SB + 2) % 3>{}, j - 6);
+        }
+    };
+
+    // ---- prologue: x row 0 (A), both weights quantized + packed (scratch: the intermediate
+    // planes, zeroed after)
+    if (isA) load_row(0, 0);
+    {
+        unsigned* red = reinterpret_cast<unsigned*>(yr);
+        unsigned* thr = red + 16;
+        scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
+        if (isA) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, 1, KS, f * 64 + lane, scale1, fin1, thr));
+        }
+        __syncthreads();
+        scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
+        if (!isA) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, 1, KS, f * 64 + lane, scale2, fin2, thr));
+        }
+        if constexpr (E != 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * (lane >> 4) + e;
+                const float s = a.ps1 ? a.ps1[c] : 1.0f;
+                ek1[e] = scale1 * s;
+                ek0[e] = (a.b1 ? a.b1[c] : 0.0f) * s + (a.pb1 ? a.pb1[c] : 0.0f);
+            }
+            const int k = lane & 15;
+            const float s2 = a.ps2 ? a.ps2[k] : 1.0f;
+            ek2s = scale2 * s2;
+            ek2b = (a.b2 ? a.b2[k] : 0.0f) * s2 + (a.pb2 ? a.pb2[k] : 0.0f);
+        } else {
+            ek2s = scale2;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw[f]));
+        if constexpr (E != 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(ek1[e]), "+v"(ek0[e]));
+        }
+        asm volatile("" : "+v"(ek2s), "+v"(ek2b));
+        __syncthreads();
+        for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
+            reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
+        if (isA && lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    for (int j = 0; j < nsteps; j += 6) {
+        step(std::integral_constant<int, 0>{}, j);
+        step(std::integral_constant<int, 1>{}, j + 1);
+        step(std::integral_constant<int, 2>{}, j + 2);
+        if (j + 3 >= nsteps) break;
+        step(std::integral_constant<int, 3>{}, j + 3);
+        step(std::integral_constant<int, 4>{}, j + 4);
+        step(std::integral_constant<int, 5>{}, j + 5);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------------------------ planning --
 struct PairPlan {
     int C = 0, waves = 0, pd = 0, nts = 0, RB = 0, nseg = 0;
@@ -650,7 +978,8 @@ void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C
     stg = 0;
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
         int v = atoi(e);
-        stg = v >= 10000 ? 1 : 0;  // + 10000: the stagger kernel (STG) where no residual is added
+        stg = v >= 20000 ? 2 : (v >= 10000 ? 1 : 0);  // + 10000: the stagger kernel (STG) where no residual is
+                                                      // added; + 20000: the role-split kernel (conv_pair_ab)
         v %= 10000;
         halves = v >= 1000 ? 1 : 0;  // + 1000: 64-byte half-line stores (C = 16)
         v %= 1000;
@@ -753,6 +1082,34 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.prio = prio;
     a.halves = halves;
     a.stg = stg;
+    if (stg == 2 && C == 16 && !residual && W <= 4 * po2q::kABSW) {
+        // role-split kernel: 2 x ceil(W / 64) waves, the pair plan's row segments
+        po2q::PairABArgs b;
+        b.N = (int)N; b.H = (int)H; b.W = (int)W;
+        b.NR = (int)((W + po2q::kABSW - 1) / po2q::kABSW);
+        b.Wp = po2q::kABSW * b.NR;
+        b.YPL = (b.Wp + 3) * 32;
+        b.RB = pp.RB; b.nseg = pp.nseg; b.items = (int)(N * pp.nseg);
+        b.remap = (pp.blocks % 8 == 0) ? 1 : 0;
+        b.q1 = a.q1; b.q2 = a.q2;
+        b.b1 = bias1; b.b2 = bias2; b.ps1 = post_scale1; b.pb1 = post_shift1; b.ps2 = post_scale2; b.pb2 = post_shift2;
+        b.act1 = act1; b.act2 = act2;
+        const size_t lds = (size_t)2 * 16 * b.Wp * 4 + (size_t)2 * 3 * b.YPL + (size_t)b.NR * 3 * po2q::kABPlane;
+        const dim3 grid((unsigned)pp.blocks), block((unsigned)(128 * b.NR));
+        const bool plain = !bias1 && !bias2 && !post_scale1 && !post_shift1 && !post_scale2 && !post_shift2 &&
+                           act1 == 0 && act2 == 0;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        if (plain)
+            hipLaunchKernelGGL((po2q::conv_pair_ab<0>), grid, block, lds, st, x, y, b);
+        else
+            hipLaunchKernelGGL((po2q::conv_pair_ab<1>), grid, block, lds, st, x, y, b);
+        const hipError_t e2 = hipGetLastError();
+        if (e2 != hipSuccess) {
+            po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e2));
+            return PO2Q_ERR_HIP;
+        }
+        return PO2Q_OK;
+    }
     const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {
         po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));

@@ -53,7 +53,7 @@ SHAPES = [(2, 20, 32, 16), (1, 9, 224, 16), (3, 37, 68, 16), (2, 1, 36, 16), (1,
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
-@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123", "1123", "10123", "10023"])
+@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123", "1123", "10123", "10023", "20023"])
 def test_pair_chain_vs_torch(shape, variant, monkeypatch):
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", variant)
     N, H, W, C = shape
@@ -186,3 +186,19 @@ def test_pair_stagger_bitwise_equal(C, W, monkeypatch):
         monkeypatch.setenv("PO2Q_PAIR_VARIANT", "10123")
         y = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
         assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("W", [224, 192, 136, 64, 8])
+def test_pair_role_split_kernel(W, monkeypatch):
+    """The role-split kernel (PO2Q_PAIR_VARIANT + 20000, conv_pair_ab: conv-1 waves and conv-2
+    waves paired on each SIMD) is bit-identical to conv_pair on the plain chain (same splits, same
+    MFMA order per accumulator) and meets the bar with BN + activation epilogues (folded affine)."""
+    x, w1, w2, e = make(2, 23, W, 29 + W, True, 16)
+    monkeypatch.setenv("PO2Q_PAIR_VARIANT", "23")
+    ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
+    monkeypatch.setenv("PO2Q_PAIR_VARIANT", "20023")
+    y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
+    assert torch.equal(y, ref)
+    y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", act1="relu", act2="silu", **e)
+    ref = torch_chain(x, w1, w2, e, "relu", "silu", None, "po2+")
+    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)

@@ -66,7 +66,10 @@ for s in $STEPS; do
                    run abc32_off_$r 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
                    run abc32_on_$r 300 env PO2Q_PAIR_C32=1 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
                done ;;
-        pairq) run pairq 300 env PAIR_C32=0 PAIR_VARIANTS=123,10123 python tools/pair_bench.py ;;
+        pairq) run pairq 300 env PAIR_C32=0 PAIR_VARIANTS=123,20023 python tools/pair_bench.py ;;
+        abab) for r in 1 2; do for v in 123 20023; do
+                   run abab_${v}_$r 300 env PO2Q_PAIR_VARIANT=$v python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar --no-models
+               done; done ;;
         benchq) run benchq 300 python bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-cifar --no-models ;;
         abstg) for r in 1 2; do for v in 123 10123 10023; do
                    run abstg_${v}_$r 300 env PO2Q_PAIR_VARIANT=$v python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar
