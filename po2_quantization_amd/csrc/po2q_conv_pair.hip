@@ -97,8 +97,9 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // at W = 112; conv 2's B fragments in LDS).  PD: x ring slots.  NTS bit 0: non-temporal
 // stores, bit 1: non-temporal x loads.
 // E: 0 = plain chain (no bias / affine / activation / residual: y = scale * acc), 1 = the
-// general epilogues (the kernel is bound by vector-instruction issue, so the plain chain
-// skips that work).
+// general epilogues, 2 = the BasicBlock form (ReLU after both BNs: the conv scale and bias folded
+// into the BN affine at staging, a compile-time ReLU; the kernel is bound by vector-instruction
+// issue, so the common forms skip that work).
 // STG 1 (stagger, MI355X_MICROARCH "two waves per SIMD" item 9): waves 4.. -- the second wave
 // of each SIMD -- run a step's conv-2 epilogue at the start of the NEXT step and split x row j
 // before their conv-2 MFMAs, so right after the barrier they issue vector work while waves
@@ -311,13 +312,17 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
-                                  : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                           : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
+                                    : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
                 if constexpr (RES) {
                     const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] += r[e];
                 }
-                if constexpr (E != 0) {
+                if constexpr (E == 2) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] < 0.0f ? 0.0f : v[e];  // ReLU (NaN propagates)
+                } else if constexpr (E != 0) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
                 }
@@ -437,6 +442,10 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                         float t;
                         if constexpr (E == 0) {
                             t = acc1[D][grp][nt][e] * scale1 + 0.0f;
+                        } else if constexpr (E == 2) {
+                            const int c = nt * 4 + e;
+                            t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
+                            t = t < 0.0f ? 0.0f : t;
                         } else {
                             const int c = nt * 4 + e;
                             t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
@@ -518,6 +527,19 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         if constexpr (!WL2) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw2[WL2 ? 0 : f]));
+        }
+        if constexpr (E == 2) {  // BasicBlock form: the conv scale and bias folded into the affine
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int c = nt * 4 + e;
+                    e1b[c] = bk1[c] * e1s[c] + e1b[c];
+                    e1s[c] = scale1 * e1s[c];
+                }
+                e2b[nt] = bk2[nt] * e2s[nt] + e2b[nt];
+                e2s[nt] = scale2 * e2s[nt];
+            }
         }
         __syncthreads();  // scratch reads done: zero the intermediate planes (padding columns, zero slots)
         for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
@@ -922,6 +944,8 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
     else if (plain)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
+    else if (res && a.act1 == 1 && a.act2 == 1)  // the BasicBlock form (resnet.py:55-71): ReLU / ReLU
+        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 2>), grid, block, pp.lds, s, x, y, a);
     else if (res)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
     else if (kStg && a.stg)

@@ -162,7 +162,7 @@ def test_pair_vs_oracle(shape, mode):
 
 @pytest.mark.parametrize("C,W", [(16, 224), (16, 96 + 32), (32, 112), (32, 64)])
 def test_pair_block_vs_oracle(C, W):
-    """The BasicBlock form BasicBlock.forward uses (E = 1 epilogues): BN affine + ReLU, conv 2,
+    """The BasicBlock form BasicBlock.forward uses (E = 2: folded affine, compile-time ReLU): BN affine + ReLU, conv 2,
     BN affine, + identity shortcut, ReLU, against the oracle chain."""
     from tests._util import normwise_err
 

@@ -95,7 +95,9 @@ for s in $STEPS; do
         sweep6) run sweep6 600 python tools/tile_sweep.py --shapes 6 --iters 21 ;;
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmcs3) run pmcs3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" s3 "conv_rowsk" all
-               python3 tools/pmc_summary.py gpurun_out/pmc_s3 > gpurun_out/pmc_s3_summary.txt 2>&1 ;;
+               python3 tools/pmc_summary.py gpurun_out/pmc_s3 177.6 > gpurun_out/pmc_s3_summary.txt 2>&1 ;;
+        pmcs2) run pmcs2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" s2 "conv_rowsf" all
+               python3 tools/pmc_summary.py gpurun_out/pmc_s2 177.6 > gpurun_out/pmc_s2_summary.txt 2>&1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;
         copyprobe) run copyprobe 300 tools/copy_probe 20 ;;
         ringprobe) run ringprobe 300 tools/copy_probe 20 1 ;;
@@ -115,7 +117,7 @@ for s in $STEPS; do
                  cp profiles/traffic.json gpurun_out/traffic.json
                  python3 tools/traffic.py gpurun_out/pmc_tpair --algorithmic 1644274688 --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
                  run pmc_pair 600 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" pair "conv_pair" all
-                 python3 tools/pmc_summary.py gpurun_out/pmc_pair > gpurun_out/pmc_pair_summary.txt 2>&1 ;;
+                 python3 tools/pmc_summary.py gpurun_out/pmc_pair 355.3 > gpurun_out/pmc_pair_summary.txt 2>&1 ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;

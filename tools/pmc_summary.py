@@ -21,7 +21,10 @@ def load(d):
     return vals
 
 
-def main(d):
+def main(d, mfma_gflop=None):
+    """mfma_gflop: the useful bf16 MFMA work of one dispatch (GFLOP, bf16x3 = 3x the conv's
+    FLOPs): adds the matrix pipe's busy fraction of the SIMD-cycles and the useful part of it
+    (one v_mfma_f32_16x16x32_bf16 = 16384 FLOP in 16 cycles)."""
     v = load(d)
     out = {k: round(x, 1) for k, x in sorted(v.items())}
     if "SQ_WAVE_CYCLES" in v:
@@ -35,8 +38,15 @@ def main(d):
         out["hbm_write_bytes"] = v["WRITE_SIZE"] * 1024
     if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v:
         out["l2_hit_rate"] = round(v["TCC_HIT_sum"] / max(1.0, v["TCC_HIT_sum"] + v["TCC_MISS_sum"]), 3)
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in v and "GRBM_GUI_ACTIVE" in v:
+        simd_cycles = 1024 * v["GRBM_GUI_ACTIVE"] / 8  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        out["mfma_busy_frac"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles, 3)
+        if mfma_gflop:
+            out["mfma_useful_frac"] = round(mfma_gflop * 1e9 / 16384 * 16 / simd_cycles, 3)
+    if "SQ_LDS_BANK_CONFLICT" in v and "SQ_LDS_IDX_ACTIVE" in v:
+        out["lds_conflict_frac"] = round(v["SQ_LDS_BANK_CONFLICT"] / max(1.0, v["SQ_LDS_IDX_ACTIVE"]), 3)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else None)
