@@ -550,7 +550,8 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
 }
 
 // The residual add inside the kernel (po2q_epi.h): the full-row plans (C = K = 16 / 32,
-// residual rows DMA'd into LDS behind the row wait) and the C = K = 32 loader-wave plans.
+// residual rows DMA'd into LDS behind the row wait), the C = K = 32 loader-wave plans and
+// every C = K = 64 plan (as its TT sibling).
 // The per-wave row kernel leaves it to the elementwise pass.
 bool rows_res_ok(const ConvPlan& p) { return rowsf_res_ok(p) || rowsk_res_ok(p); }
 
@@ -558,8 +559,7 @@ hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_
                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
                                 int act, hipStream_t s, const WQuant& q) {
     if (rowsf_res_ok(p)) return launch_conv_rowsf_res(p, x, packed, scale, bias, y, ps, pb, res, act, s, q);
-    if (p.fp) return hipErrorInvalidValue;
-    if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s);
+    if (rowsk_res_ok(p)) return launch_conv_rowsk_res(p, x, packed, scale, bias, y, ps, pb, res, act, s, q);
     return hipErrorInvalidValue;
 }
 

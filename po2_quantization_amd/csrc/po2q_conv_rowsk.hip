@@ -157,8 +157,9 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 // Product builds: DBG = 0.
 // NTS (plan field nts, autotune candidates): bit 0 = output stores, bit 1 = x loads with
 // the non-temporal policy
-// RES (with LW, TT, EPI): the residual add inside the kernel (the loader wave DMAs the
-//     residual rows next to the output tile; act after the add)
+// RES (with TT, EPI): the residual add inside the kernel (the loader wave -- or, without
+//     LW, each MFMA wave for the channels its tile stores cover -- DMAs the residual rows
+//     into a 2-slot ring next to the output tile; act after the add)
 // FP (plan field fp, not with LW): the block reduces max|w| and each wave quantizes +
 //     packs its own VGPR-resident B fragments (po2q_quant_dev.h wq_*): one launch per layer
 template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, int NTS = 0, bool RES = false,
@@ -303,10 +304,32 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         for (int i = 0; i < DPW; ++i) rows_dma16<(NTS & 2) != 0>(rs, vo, i * soff1, base + (uint32_t)(DPW * wave + i) * 1024u);
         rows_dma4<(NTS & 2) != 0>(rs, voh, base + (uint32_t)RAWI + (uint32_t)wave * 256u);
     };
+    // RES without LW: per step this wave first DMAs the residual of the row its store_tile
+    // writes in the NEXT step (NR instructions, the channels of that store), then the x row
+    constexpr int NR = (RES && !LW) ? NGW : 0;
+    static_assert(!RES || TT, "the residual rides on the TT output tile");
     // vm ops issued after a row's DMAs (step j-PD) until row j is split: that step's
-    // stores, then per later step the DMAs of one more row and that step's stores
-    constexpr int VMW = (PD - 1) * (DPW + 1 + NGW) + NGW;
+    // stores, then per later step the residual and x DMAs of one more row and that step's stores
+    constexpr int VMW = (PD - 1) * (NR + DPW + 1 + NGW) + NGW;
+    // vm ops issued after the residual DMAs of step j-1 until step j's store_tile: step j-1's
+    // x DMAs and stores, step j's residual and x DMAs
+    constexpr int RW = 2 * (DPW + 1) + NGW + NR;
     const int PQ = a.P * a.Q;
+    const __amdgpu_buffer_rsrc_t rres = rows_rsrc(NR ? a.res + (int64_t)n * K * PQ : x, NR ? K * PQ * 4 : 4);
+    const uint32_t vr0 = (uint32_t)((K / 4) * wave + (lane >> 3)) * (uint32_t)PQ * 4u + (uint32_t)gq4 * 4u;
+    // the residual row store_tile writes in step js (output row p0 + js - 3) into slot js & 1,
+    // [K][32 columns] unswizzled: instruction i, lane l -> channel (K/4)w + 8i + (l >> 3)
+    auto load_res = [&](int js) __attribute__((always_inline)) {
+        if constexpr (NR != 0) {
+            const int orow = js - 3;
+            const bool ok = orow >= 0 && orow < rbe && gq4 < a.Q;
+            const uint32_t vo = ok ? vr0 + (uint32_t)(p0 + orow) * (uint32_t)a.Q * 4u : 0x7fffffffu;
+            const uint32_t base = (uint32_t)(uintptr_t)resb + (uint32_t)((js & 1) * kKTile<C>) +
+                                  (uint32_t)((K / 4) * wave) * (kKSW * 4u);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) rows_dma16(rres, vo, i * 8u * (uint32_t)PQ * 4u, base + (uint32_t)i * 1024u);
+        }
+    };
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * K * PQ, K * PQ * 4);
 
     // TT stores: wave w, instruction i: lane l -> channel (K/4)w + 8i + (l >> 3), columns
@@ -375,7 +398,10 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         // refill the raw slot this wave just split (its own data only)
-        if constexpr (!(DBG & 128) && !LW) load_row(std::integral_constant<int, RS>{}, j + PD);
+        if constexpr (!(DBG & 128) && !LW) {
+            load_res(j + 1);
+            load_row(std::integral_constant<int, RS>{}, j + PD);
+        }
         // MFMAs: halo row j feeds output halo-index j+1 (r=0), j (r=1), j-1 (r=2)
         constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
 #pragma unroll
@@ -406,6 +432,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             // store the row completed in the previous step (tile 1 - B2, published by
             // this step's barrier), then park this step's row in tile B2
             // (the loop runs whole triples of steps: steps past nrows - 1 only store)
+            if constexpr (NR != 0) rows_wait<RW>();  // this row's residual (DMA'd in step j - 1)
             store_tile(tile + (1 - B2) * kKTile<C>, p0 + j - 3, j >= 3 && j - 3 < rbe, B2);
             unsigned char* tw = tile + B2 * kKTile<C>;
 #pragma unroll
@@ -441,6 +468,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
     {
         const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
         auto pre = [&](auto R_) __attribute__((always_inline)) {
+            load_res(decltype(R_)::value - PD + 1);  // no output row yet: counted, out of range
             load_row(R_, decltype(R_)::value);
 #pragma unroll
             for (int i = 0; i < NGW; ++i) rows_store<(NTS & 1) != 0>(ry, 0x7fffffffu, z);
@@ -465,6 +493,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
     if (TT && nrows % 3 == 0) {
         // the last row (parked by step nrows - 1; with nrows % 3 != 0 the loop's extra
         // step nrows has stored it)
+        if constexpr (NR != 0) rows_wait<0>();  // the flushed row's residual
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         store_tile(tile + ((nrows - 1) & 1) * kKTile<C>, p0 + rbe - 1, true, nrows & 1);
@@ -630,14 +659,27 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     return hipErrorInvalidValue;
 }
 
-// The residual add inside the kernel: the loader-wave plans of C = K = 32 (po2q_epi.h).
+// The residual add inside the kernel (po2q_epi.h): the loader-wave plans of C = K = 32, and
+// every C = K = 64 plan -- run as its TT sibling with 2 ring slots (the residual ring makes
+// it 2 blocks per CU: 77 KiB of LDS) -- instead of the conv plus an elementwise pass over y
+// (the BasicBlock conv2 of ResNet56 stage 3, reference models/resnet.py:69-71).
+static bool rowsk64_res_on() {
+    static const bool on = [] {
+        const char* e = getenv("PO2Q_ROWSK_RES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool rowsk_res_ok(const ConvPlan& p) {
-    return p.kind == KIND_BF16X3_ROWS && p.vrx == 3 && p.C == 32 && p.K == 32 && p.pd == 3;
+    if (p.kind != KIND_BF16X3_ROWS) return false;
+    if (p.C == 32 && p.K == 32) return p.vrx == 3 && p.pd == 3 && !p.fp;
+    return p.C == 64 && p.K == 64 && (p.vrx == 1 || p.vrx == 2) && rowsk64_res_on();
 }
 
 hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                 int act, hipStream_t s) {
+                                 int act, hipStream_t s, const WQuant& q) {
     if (!rowsk_res_ok(p) || !res) return hipErrorInvalidValue;
     RowsKArgs a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
@@ -648,6 +690,19 @@ hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16
     a.pb = pb;
     a.act = act;
     a.res = res;
+    a.q = q;
+    if (p.C == 64) {
+        constexpr size_t lds64 = kKLds<64, 2, true> + 2 * kKTile<64>;
+        if (p.fp) {
+            if (!q.w) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((conv_rowsk<64, 2, true, false, true, 0, 0, true, true>), dim3((unsigned)p.blocks),
+                               dim3(kThreads), lds64, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+        } else {
+            hipLaunchKernelGGL((conv_rowsk<64, 2, true, false, true, 0, 0, true>), dim3((unsigned)p.blocks),
+                               dim3(kThreads), lds64, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a);
+        }
+        return hipGetLastError();
+    }
     const size_t lds = p.lds_bytes + 2 * kKTile<32>;
 #define PO2Q_RKR(nt)                                                                                         \
     if (p.nts == nt) {                                                                                       \

@@ -26,9 +26,10 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 }
 
 // Row-streaming kernels with the affine map + activation in their store epilogue
-// (po2q_conv_rows.hip / po2q_conv_rowsk.hip); the residual is left to launch_epilogue.
-// the residual add in the kernel too: rows_res_ok / launch_conv_rows_res cover every
-// plan that can (po2q_conv_rows.hip), the rowsk_* pair the loader-wave plans
+// (po2q_conv_rows.hip / po2q_conv_rowsk.hip); the residual add in the kernel too where the
+// plan can: rows_res_ok / launch_conv_rows_res (po2q_conv_rows.hip) cover the full-row
+// plans, rowsk_res_ok / launch_conv_rowsk_res the C = 32 loader-wave and every C = 64 plan;
+// any other plan leaves the residual to launch_epilogue.
 bool rows_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                 const float* bias, float* y, const float* ps, const float* pb, const float* res,
@@ -36,7 +37,7 @@ hipError_t launch_conv_rows_res(const ConvPlan& p, const float* x, const uint16_
 bool rowsk_res_ok(const ConvPlan& p);
 hipError_t launch_conv_rowsk_res(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                                  const float* bias, float* y, const float* ps, const float* pb, const float* res,
-                                 int act, hipStream_t s);
+                                 int act, hipStream_t s, const WQuant& q = WQuant{});
 hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const uint16_t* packed,
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s, const WQuant& q = WQuant{});

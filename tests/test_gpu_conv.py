@@ -351,6 +351,46 @@ def test_fused_epilogue_every_candidate_plan(shape, monkeypatch):
             assert err <= CONV_TOL, (i, act, err)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 5, 56), (1, 64, 6, 40), (3, 64, 7, 8), (1, 64, 12, 36), (2, 64, 1, 60)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_c64_residual_in_kernel_every_plan_vs_oracle(shape, monkeypatch):
+    """The BasicBlock conv2 of ResNet56 stage 3 (resnet.py:69-71: bn2(conv2(h)) + shortcut, ReLU)
+    through the C = 64 row kernel's in-kernel residual (every candidate plan runs as its TT
+    sibling with the residual ring; row counts cover every flush case of the 3-step unroll), against
+    the oracle's fp64 conv of the bit-exact Q(w) with numpy affine / residual / ReLU."""
+    N, C, H, W = shape
+    g = torch.Generator().manual_seed(H * 100 + W)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) * 0.06
+    ps = torch.rand(C, generator=g) + 0.5
+    pb = torch.randn(C, generator=g) * 0.1
+    res = torch.randn(N, C, H, W, generator=g)
+    conv, _ = O.qconv2d(x.numpy(), w.numpy(), None, 1, 1, 1, 1, 4, "po2")
+    ref = np.maximum(conv * ps.numpy().astype(np.float64).reshape(1, -1, 1, 1)
+                     + pb.numpy().astype(np.float64).reshape(1, -1, 1, 1) + res.numpy().astype(np.float64), 0.0)
+    xd, wd, psd, pbd, rd = (t.to(DEV) for t in (x, w, ps, pb, res))
+    n = len(_lib.plans(N, C, H, W, C, 3, 3, 1, 1))
+    for i in range(n):
+        monkeypatch.setenv("PO2Q_PLAN", str(i))
+        y = _lib.qconv2d_fused(xd, wd, None, 1, 1, post_scale=psd, post_shift=pbd, residual=rd, act="relu")
+        err = normwise_err(y.cpu().numpy(), ref)
+        assert err <= CONV_TOL, (i, _lib.plans(N, C, H, W, C, 3, 3, 1, 1)[i], err)
+
+
+def test_c64_residual_in_kernel_full_size():
+    """bs = 256 @56 (the BASELINE config's stage 3) with the in-kernel residual, against torch fp32."""
+    torch.manual_seed(5)
+    x = torch.relu(torch.randn(256, 64, 56, 56, device=DEV))
+    w = torch.randn(64, 64, 3, 3, device=DEV) * 0.06
+    ps = torch.rand(64, device=DEV) + 0.5
+    pb = torch.randn(64, device=DEV) * 0.1
+    res = torch.randn(256, 64, 56, 56, device=DEV)
+    y = _lib.qconv2d_fused(x, w, None, 1, 1, post_scale=ps, post_shift=pb, residual=res, act="relu")
+    ref = torch.relu(torch.nn.functional.conv2d(x, _lib.quantize(w, 4, "po2"), None, 1, 1) * ps.view(1, -1, 1, 1)
+                     + pb.view(1, -1, 1, 1) + res)
+    assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL
+
+
 NONFINITE_SHAPES = [(2, 16, 12, 224, 16, 3, 1, 1), (2, 32, 10, 112, 32, 3, 1, 1), (2, 64, 9, 56, 64, 3, 1, 1),
                     (2, 16, 11, 64, 32, 3, 2, 1), (2, 32, 8, 32, 64, 1, 2, 0), (2, 24, 6, 6, 144, 1, 1, 0)]
 

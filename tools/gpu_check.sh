@@ -54,6 +54,9 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/dwtests.log || grep -q "failed\|error" gpurun_out/dwtests.log; then
                    echo "stopping: depthwise GPU tests did not pass"; exit 1
                fi ;;
+        c64res) run c64res 600 python -u -m pytest tests/test_gpu_conv.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c64_residual or fused_epilogue"
+               if ! grep -q " passed" gpurun_out/c64res.log || grep -q "failed\|error" gpurun_out/c64res.log; then
+                   echo "stopping: c64res failed"; exit 3; fi ;;
         pairtests) run pairtests 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -q --timeout 300 --timeout-method thread
                if ! grep -q " passed" gpurun_out/pairtests.log || grep -q "failed\|error" gpurun_out/pairtests.log; then
                    echo "stopping: pair GPU tests did not pass"; exit 1
