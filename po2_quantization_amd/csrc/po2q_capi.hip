@@ -211,6 +211,8 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         const uint16_t* pk = reinterpret_cast<const uint16_t*>(packed);
         if (p.kind == KIND_BF16X3_PW)  // affine, residual and activation all in the kernel's stores
             return hip_status(launch_conv_pw(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s), "conv launch");
+        if (p.kind == KIND_BF16X3_IMG)  // the same
+            return hip_status(launch_conv_img(p, x, pk, scale, bias, y, e.ps, e.pb, e.res, e.act, s), "conv launch");
         hipError_t he;
         bool fused_affine = false;
         if (p.kind == KIND_BF16X3_DMA) {
@@ -250,7 +252,7 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
 }
 
 static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows", "bf16x3_pw",
-                                   "direct_f32", "pw_f32"};
+                                   "direct_f32", "pw_f32", "bf16x3_img"};
 
 static void describe_plan(const ConvPlan& p, char* buf, size_t len) {
     snprintf(buf, len,

@@ -299,6 +299,12 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
             std::vector<PlanCand> pwc;
             pw_candidates(p, mode, bits, fsr, pwc);
             if (!pwc.empty() && !tuning_knobs()) p = pwc[0].plan;
+            // small images (CIFAR sizes): the LDS-resident block kernel; its candidates ride on
+            // the pointwise list (the two never apply to the same shape)
+            if (pwc.empty()) {
+                img_candidates(p, mode, bits, fsr, pwc);
+                if (!pwc.empty() && p.W <= 32 && !tuning_knobs()) p = pwc[0].plan;
+            }
             if (pw_out) *pw_out = std::move(pwc);
             if (rows_out) *rows_out = std::move(rows);
             if (reg_out) *reg_out = std::move(reg);
@@ -359,11 +365,12 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             for (const ConvPlan& o : out)
                 dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
                        o.dma_waves == c.dma_waves && o.dma_ov == c.dma_ov &&
-                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS && o.fp == c.fp;
+                       o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS && o.fp == c.fp &&
+                       (c.kind != KIND_BF16X3_IMG || o.kblocks == c.kblocks);
             if (!dup) out.push_back(c);
         }
     };
-    add(pwc, 8);
+    add(pwc, 12);
     add(rows, kTuneRowsCands);
     add(reg, kTuneRegCands);
     add(dma, kTuneDmaCands);

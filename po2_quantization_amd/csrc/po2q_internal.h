@@ -35,12 +35,14 @@ enum ConvKind {
     KIND_BF16X3_ROWS = 4,
     KIND_BF16X3_PW = 5,  // 1x1 / stride 1 GEMM kernel (po2q_conv_pw.hip)
     KIND_DIRECT_F32 = 6,  // unquantized 3-channel stems, direct fp32 (po2q_conv_f32s.hip)
-    KIND_PW_F32 = 7       // unquantized 1x1 convs, fp32 MFMA GEMM (po2q_conv_f32s.hip)
+    KIND_PW_F32 = 7,      // unquantized 1x1 convs, fp32 MFMA GEMM (po2q_conv_f32s.hip)
+    KIND_BF16X3_IMG = 8   // 3x3 / stride 1, small images: the block's rows resident in LDS (po2q_conv_img.hip)
 };
 
 // Every kind whose weight is packed as exact bf16 +-2^e fragments + one fp32 scale.
 inline bool is_bf16x3_kind(int kind) {
-    return kind == KIND_BF16X3 || kind == KIND_BF16X3_DMA || kind == KIND_BF16X3_ROWS || kind == KIND_BF16X3_PW;
+    return kind == KIND_BF16X3 || kind == KIND_BF16X3_DMA || kind == KIND_BF16X3_ROWS || kind == KIND_BF16X3_PW ||
+           kind == KIND_BF16X3_IMG;
 }
 
 // Conv geometry and tiling plan (host-side, shared by workspace sizing and launch).
@@ -127,6 +129,13 @@ void pw_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
 hipError_t launch_conv_pw(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
                           const float* bias, float* y, const float* ps, const float* pb, const float* res, int act,
                           hipStream_t s);
+
+// Small-image 3x3 / stride-1 candidates (po2q_conv_img.hip), cost-ranked; empty if not eligible.
+void img_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vector<PlanCand>& out);
+// Its launch (row-kernel pack layout), the eval epilogue (ps / pb / res may be NULL) in the store.
+hipError_t launch_conv_img(const ConvPlan& p, const float* x, const uint16_t* packed, const float* scale,
+                           const float* bias, float* y, const float* ps, const float* pb, const float* res, int act,
+                           hipStream_t s);
 
 // fp32 kernels for mode none (po2q_conv_f32s.hip): candidates (empty if not eligible) and the
 // launch with the eval epilogue in the store; the weight is read as given (no pack).

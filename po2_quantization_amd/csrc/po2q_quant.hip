@@ -310,7 +310,7 @@ static PackX3 pack_geom(const ConvPlan& p) {
     PackX3 pg;
     pg.C = p.C; pg.K = p.K; pg.R = p.R; pg.S = p.S; pg.CC = p.CC; pg.NT = p.NT;
     pg.nchunks = p.nchunks; pg.ksteps = p.steps; pg.taps = p.taps;
-    pg.vr = p.kind == KIND_BF16X3_ROWS ? 2 : (p.vrx ? 1 : 0);
+    pg.vr = (p.kind == KIND_BF16X3_ROWS || p.kind == KIND_BF16X3_IMG) ? 2 : (p.vrx ? 1 : 0);
     pg.total = p.packed_floats * 2;
     return pg;
 }

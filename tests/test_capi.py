@@ -138,3 +138,17 @@ def test_plan_enumeration_on_host():
     assert L.po2q_qconv2d_f32_plan(99, 1, 1, None, 1, 2, 16, 10, 10, 16, 3, 3, 1, 1, 1, 1, 1, 1, 1, 4, 1, 1, 0,
                                    1, 1 << 20, None) == 1
     assert b"out of range" in L.po2q_last_error()
+
+
+def test_small_image_plans_on_host():
+    """CIFAR-size 3x3 / stride-1 convs (ResNet56 @32: 32x32 x 16, 16x16 x 32, 8x8 x 64) default to
+    the LDS-resident small-image kernel and offer its row-segment / channel-group variants to the
+    autotuner; ImageNet-size rows keep the row kernels."""
+    for C, H in ((16, 32), (32, 16), (64, 8)):
+        shape = dict(N=256, C=C, H=H, W=H, K=C, R=3, S=3, stride=1, padding=1)
+        ps = _lib.plans(**shape)
+        assert "kind=bf16x3_img" in _lib.describe(**shape), _lib.describe(**shape)
+        assert sum("kind=bf16x3_img" in p for p in ps) >= 2
+        assert len(set(ps)) == len(ps)
+    assert not any("bf16x3_img" in p for p in _lib.plans(256, 16, 224, 224, 16, 3, 3, 1, 1))
+    assert not any("bf16x3_img" in p for p in _lib.plans(2, 16, 10, 10, 16, 3, 3, 1, 1))  # W % 4 != 0

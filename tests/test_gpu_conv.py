@@ -391,6 +391,40 @@ def test_c64_residual_in_kernel_full_size():
     assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL
 
 
+IMG_SHAPES = [(2, 16, 32, 32, 16), (2, 32, 16, 16, 32), (3, 64, 8, 8, 64), (1, 64, 7, 12, 64), (2, 32, 5, 8, 16),
+              (2, 16, 9, 20, 32), (1, 64, 3, 4, 32), (2, 16, 1, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", IMG_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_small_image_kernel_every_plan_vs_oracle(shape, monkeypatch):
+    """The small-image kernel (po2q_conv_img.hip) through every one of its candidate plans (row
+    segments, output-channel groups), plain and with the eval epilogue + residual, against the
+    oracle's fp64 conv of the bit-exact Q(w): ragged row counts, groups spanning rows, K != C."""
+    N, C, H, W, K = shape
+    g = torch.Generator().manual_seed(N * 1000 + C * 10 + H)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(K, C, 3, 3, generator=g) * 0.1
+    ps = torch.rand(K, generator=g) + 0.5
+    pb = torch.randn(K, generator=g) * 0.1
+    res = torch.randn(N, K, H, W, generator=g)
+    conv, _ = O.qconv2d(x.numpy(), w.numpy(), None, 1, 1, 1, 1, 4, "po2+")
+    v = lambda t: t.numpy().astype(np.float64).reshape(1, -1, 1, 1)  # noqa: E731
+    ref_epi = np.clip(conv * v(ps) + v(pb) + res.numpy().astype(np.float64), 0.0, 6.0)
+    xd, wd, psd, pbd, rd = (t.to(DEV) for t in (x, w, ps, pb, res))
+    plans = _lib.plans(N, C, H, W, K, 3, 3, 1, 1, mode="po2+")
+    idx = [i for i, p in enumerate(plans) if "kind=bf16x3_img" in p]
+    assert idx, plans
+    for i in idx:
+        monkeypatch.setenv("PO2Q_PLAN", str(i))
+        y = _lib.qconv2d(xd, wd, None, 1, 1, 1, 1, 4, "po2+")
+        err = normwise_err(y.cpu().numpy(), conv)
+        assert err <= CONV_TOL, (plans[i], err)
+        y = _lib.qconv2d_fused(xd, wd, None, 1, 1, 1, 1, 4, "po2+", post_scale=psd, post_shift=pbd, residual=rd,
+                               act="relu6")
+        err = normwise_err(y.cpu().numpy(), ref_epi)
+        assert err <= CONV_TOL, (plans[i], "epilogue", err)
+
+
 NONFINITE_SHAPES = [(2, 16, 12, 224, 16, 3, 1, 1), (2, 32, 10, 112, 32, 3, 1, 1), (2, 64, 9, 56, 64, 3, 1, 1),
                     (2, 16, 11, 64, 32, 3, 2, 1), (2, 32, 8, 32, 64, 1, 2, 0), (2, 24, 6, 6, 144, 1, 1, 0)]
 

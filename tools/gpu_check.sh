@@ -90,6 +90,7 @@ for s in $STEPS; do
         bench32) run bench32 600 python bench.py --image 32 --steps 20 --warmup 3 --no-cpu-baseline ;;
         bench32g) run bench32g 600 python bench.py --image 32 --steps 50 --warmup 3 --graph --no-cpu-baseline ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
+        sweepc) run sweepc 600 python tools/tile_sweep.py --shapes 7,8,9 --iters 21 ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep1) run sweep1 600 python tools/tile_sweep.py --shapes 1 --iters 21 ;;
         sweep4) run sweep4 600 python tools/tile_sweep.py --shapes 4 --iters 21 ;;

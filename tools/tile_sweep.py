@@ -13,7 +13,9 @@ sys.path.insert(0, ROOT)
 from po2_quantization_amd import _lib  # noqa: E402
 
 SHAPES = [(16, 224, 16, 3, 1, 1), (16, 224, 32, 3, 2, 1), (16, 224, 32, 1, 2, 0), (32, 112, 32, 3, 1, 1),
-          (32, 112, 64, 3, 2, 1), (32, 112, 64, 1, 2, 0), (64, 56, 64, 3, 1, 1)]
+          (32, 112, 64, 3, 2, 1), (32, 112, 64, 1, 2, 0), (64, 56, 64, 3, 1, 1),
+          # ResNet56 @32 (config 2) stride-1 shapes: indices 7, 8, 9
+          (16, 32, 16, 3, 1, 1), (32, 16, 32, 3, 1, 1), (64, 8, 64, 3, 1, 1)]
 
 
 def timeit(fn, iters):
