@@ -253,6 +253,35 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
                           void* stream);
 
 /*
+ * A chain of n_layers quantized 3x3 / stride-1 / pad-1 C -> C convs on small images in ONE
+ * launch: the stride-1 run of a ResNet stage at CIFAR size -- consecutive
+ * QuantizedConv2d.forward calls (models/quantized_conv.py:32-38) as models/resnet.py:55-71 /
+ * 25-50 chain them, each with its BasicBlock's eval BN / ReLU / identity shortcut:
+ *   a_0 = x;  a_{l+1} = act[l]((conv(a_l, Q(w[l])) + bias[l]) * post_scale[l] + post_shift[l]
+ *                              (+ a_{res_from[l]} when res_from[l] >= 0));  y = a_{n_layers}
+ * w, bias, post_scale, post_shift: host arrays of n_layers DEVICE pointers (the three epilogue
+ * arrays, and any entry of them, may be NULL: skipped); act, res_from: host arrays (NULL: none;
+ * res_from[l] in [-1, l], the residual is layer res_from[l]'s input).  Every weight is
+ * [C, C, 3, 3], quantized with its own max|w| and the same (bits, fsr, mode).
+ * One block per image runs every layer with the activation resident in LDS (only x is read and
+ * y written); the weights are quantized + packed by batched launches first (the workspace holds
+ * the packs).  The residual sources are held one at a time: two layers adding DIFFERENT sources
+ * must not overlap (source <= the earlier user) -- the BasicBlock pattern [-1, 0, -1, 2, ...] and
+ * any chain without residuals qualify.  Takes C in {16, 32, 64}, W % 4 == 0,
+ * 1 <= n_layers <= PO2Q_CHAIN_MAX_LAYERS, (H + 2)(W + 2) 6C bytes <= 160 KiB and H * W <= 1024
+ * (C = 16), 256 (C = 32), 128 (C = 64) -- ResNet's CIFAR stages --, mode po2 / po2+ with the
+ * exponent window inside bf16's range.
+ */
+#define PO2Q_CHAIN_MAX_LAYERS 24
+int po2q_qconv2d_chain_supported(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers, int bits, int fsr,
+                                 int mode);
+size_t po2q_qconv2d_chain_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers);
+int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* const* bias,
+                           const float* const* post_scale, const float* const* post_shift, const int* act,
+                           const int* res_from, int n_layers, int64_t N, int64_t C, int64_t H, int64_t W, int bits,
+                           int fsr, int mode, float* y, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * The stride-2 transition of a ResNet56 stage (reference models/resnet.py:55-71 with the
  * projection shortcut: conv1 = QuantizedConv2d(C, 2C, 3, stride 2, padding 1) and
  * downsample.0 = QuantizedConv2d(C, 2C, 1, stride 2, padding 0), both
@@ -304,7 +333,7 @@ void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan);
  * QuantizedConv2d.forward quantizes its weight, models/quantized_conv.py:32-38): for every
  * plans[i] whose kernel does not stage its weight itself, quantize + pack w[i] into
  * workspace[i] (>= po2q_qconv2d_plan_workspace_bytes) -- the bf16x3 packs in
- * ceil(n / 16) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
+ * ceil(n / 24) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
  * from that workspace (w is read only by plans that stage their weight in-kernel); on one
  * stream the pair equals po2q_qconv2d_plan_run bit for bit.
  */

@@ -58,6 +58,9 @@ EXPORTS = (
     "po2q_qconv2d_plan_pack_batch",
     "po2q_qconv2d_plan_run_packed",
     "po2q_dilate_f32",
+    "po2q_qconv2d_chain_supported",
+    "po2q_qconv2d_chain_workspace_bytes",
+    "po2q_qconv2d_chain_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -159,6 +162,12 @@ def load():
                                                ctypes.POINTER(sz), p]
     L.po2q_qconv2d_plan_run_packed.restype = i32
     L.po2q_qconv2d_plan_run_packed.argtypes = [p] * 8 + [i32, p, sz, p]
+    L.po2q_qconv2d_chain_supported.restype = i32
+    L.po2q_qconv2d_chain_supported.argtypes = [i64] * 4 + [i32] * 4
+    L.po2q_qconv2d_chain_workspace_bytes.restype = sz
+    L.po2q_qconv2d_chain_workspace_bytes.argtypes = [i64] * 4 + [i32]
+    L.po2q_qconv2d_chain_f32.restype = i32
+    L.po2q_qconv2d_chain_f32.argtypes = ([p] * 7 + [i32] + [i64] * 4 + [i32] * 3 + [p, p, sz, p])
     _lib = L
     return L
 
@@ -460,11 +469,75 @@ def qconv2d_pair(x, w1, w2, bits=4, mode="po2", fsr=1, bias1=None, bias2=None, p
                     post_shift1, ACTS[act1], post_scale2, post_shift2, residual, ACTS[act2])
 
 
+CHAIN_MAX_LAYERS = 24  # include/po2q.h PO2Q_CHAIN_MAX_LAYERS
+
+
+def chain_supported(x_shape, n_layers, bits=4, mode="po2", fsr=1):
+    """Whether qconv2d_chain takes n_layers C -> C 3x3 / stride-1 convs on x of this shape
+    (po2q_qconv2d_chain_supported: C in {16, 32, 64}, W % 4 == 0, the padded image's split planes
+    in LDS -- CIFAR sizes)."""
+    N, C, H, W = (int(v) for v in x_shape)
+    return bool(load().po2q_qconv2d_chain_supported(N, C, H, W, int(n_layers), int(bits), int(fsr),
+                                                     MODES[mode]))
+
+
+def qconv2d_chain(x, weights, bits=4, mode="po2", fsr=1, biases=None, post_scales=None, post_shifts=None,
+                  acts=None, res_from=None):
+    """len(weights) quantized 3x3 / stride-1 / pad-1 C -> C convs in ONE launch (po2q_qconv2d_chain_f32):
+        a_0 = x;  a_{l+1} = act_l((conv(a_l, Q(w_l)) + bias_l) * post_scale_l + post_shift_l
+                                  (+ a_{res_from[l]}));   returns a_L
+    -- the stride-1 run of a ResNet stage at CIFAR size, QuantizedConv2d.forward after
+    QuantizedConv2d.forward as models/resnet.py:55-71 chains them (BN folded into the affine, the
+    identity shortcut as res_from = the block's first layer).  None entries / lists: skipped."""
+    _require_hip_f32(x, "input")
+    n = len(weights)
+    for i, w in enumerate(weights):
+        _require_hip_f32(w, "weight %d" % i)
+    L = load()
+    xc = x.contiguous()
+    N, C, H, W = (int(v) for v in xc.shape)
+    ws_ = [w.contiguous() for w in weights]
+    for i, w in enumerate(ws_):
+        if tuple(w.shape) != (C, C, 3, 3):
+            raise Po2qError("po2q: chain weight %d must be [%d, %d, 3, 3], got %s" % (i, C, C, tuple(w.shape)))
+
+    def ptrs(ts, what):
+        if ts is None:
+            return None, []
+        keep = []
+        arr = (ctypes.c_void_p * n)()
+        for i, t in enumerate(ts):
+            if t is None:
+                arr[i] = None
+                continue
+            _require_hip_f32(t, "%s %d" % (what, i))
+            tc = t.contiguous()
+            if tc.numel() != C:
+                raise Po2qError("po2q: chain %s %d must have %d elements" % (what, i, C))
+            keep.append(tc)
+            arr[i] = tc.data_ptr()
+        return arr, keep
+
+    wa = (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws_])
+    ba, kb = ptrs(biases, "bias")
+    sa, ks = ptrs(post_scales, "post_scale")
+    ha, kh = ptrs(post_shifts, "post_shift")
+    aa = (ctypes.c_int * n)(*[ACTS[a] for a in acts]) if acts is not None else None
+    ra = (ctypes.c_int * n)(*[-1 if r is None else int(r) for r in res_from]) if res_from is not None else None
+    y = torch.empty_like(xc)
+    nbytes = L.po2q_qconv2d_chain_workspace_bytes(N, C, H, W, n)
+    ws = _workspace(nbytes, xc.device)
+    _check(L.po2q_qconv2d_chain_f32(xc.data_ptr(), wa, ba, sa, ha, aa, ra, n, N, C, H, W, int(bits), int(fsr),
+                                    MODES[mode], y.data_ptr(), ws.data_ptr(), max(int(nbytes), 256),
+                                    _stream(xc.device)))
+    return y
+
+
 class PackedConvs:
     """Several QuantizedConv2d forwards (models/quantized_conv.py:32-38) with their weight
     quantize + pack as ONE batched launch (po2q_qconv2d_plan_pack_batch) and each conv from its
     packed workspace (po2q_qconv2d_plan_run_packed) -- the same kernels and results as
-    qconv2d() layer by layer, with ceil(n / 16) pack launches instead of one per layer.
+    qconv2d() layer by layer, with ceil(n / 24) pack launches instead of one per layer.
 
     specs: [(x_shape, w, stride, padding)] in call order (groups 1, dilation 1, no bias); the
     plans are resolved once here, so create it after the shapes were autotuned.  Call pack()

@@ -1,0 +1,477 @@
+// A chain of quantized 3x3 / stride-1 / pad-1 C -> C convs on SMALL images, all of them in ONE
+// launch: the stride-1 run of a ResNet56 stage at CIFAR size (reference models/resnet.py:55-71,
+// 25-50; each conv QuantizedConv2d.forward, models/quantized_conv.py:32-38), with each layer's
+// eval BN affine, activation and the BasicBlock's identity shortcut in its store.
+//
+// Why: at 32x32 / 16x16 / 8x8 a layer is 4-17 MB and its arithmetic a microsecond or two of
+// MFMA time per CU, so one launch per layer spends most of its ~10 us in the launch, the first
+// load's latency, the store drain -- and, even in one launch, in the global round trip of every
+// activation (profiles/r03_cifar32_kernel_stats.csv).  Images are independent through the whole
+// stage, so a block owns ONE image for every layer, and the activation never leaves the CU:
+//   start:      x -> exact hi / mid / lo bf16 split planes [(H + 2) x (W + 2) padded pixels][C]
+//               in LDS (zero halo), one batch of independent loads per thread;
+//   per layer:  every wave computes ALL its 16-pixel groups' accumulators for its 16-channel
+//               output tile (B fragments from the layer's pack, the row-kernel layout; the
+//               transposed MFMA form, so a lane ends with 4 consecutive channels of one pixel),
+//               barrier (every read of the input planes retired), epilogue (bias, eval BN
+//               affine, + the held residual, activation), split, and the planes are overwritten
+//               IN PLACE (3 ds_write_b64), barrier; the last layer stores y instead.
+//   residual:   a BasicBlock's input is held in VGPRs by the lanes that add it two layers later
+//               (every layer maps (wave, lane) to the same pixel and channels).
+// The weights of all layers are quantized + packed by batched pack launches first.  Same
+// arithmetic as every bf16x3 kernel (exact +-2^e bf16 weights, exact 3-way split of the fp32
+// activations -- each layer's fp32 output re-split exactly --, fp32 accumulation on
+// v_mfma_f32_16x16x32_bf16).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "../../include/po2q.h"
+#include "po2q_epi.h"
+#include "po2q_internal.h"
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+namespace {
+constexpr int kChainThreads = 512;  // 8 waves: two per SIMD
+constexpr int kChainItems = 5;      // split items (pixel x channel octet) per thread and load batch
+constexpr int kChainMax = PO2Q_CHAIN_MAX_LAYERS;
+constexpr size_t kChainLdsMax = 160 * 1024;
+
+template <int C>
+__device__ __forceinline__ int ch_addr(int pp, int oc) {
+    if constexpr (C == 16)
+        return pp * 32 + 16 * (oc ^ ((pp >> 3) & 1));
+    else if constexpr (C == 32)
+        return pp * 64 + 16 * (oc ^ ((pp >> 2) & 3));
+    else
+        return pp * 128 + 16 * (oc ^ ((pp >> 1) & 7));
+}
+
+size_t chain_plane(int64_t C, int64_t H, int64_t W) { return (size_t)((H + 2) * (W + 2) * 2 * C + 16); }
+
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+}  // namespace
+
+struct ChainLayer {
+    const uint4* wp;      // packed B fragments [r][ks][nt][lane] (row-kernel layout)
+    const float* scale;   // the layer's max|w| multiplier
+    const float* bias;    // [C] or NULL
+    const float* ps;      // eval BN affine [C] or NULL
+    const float* pb;
+    int act;              // PO2Q_ACT_*
+    int res_add;          // 1: + the held residual (a BasicBlock's input) before the activation
+    int keep;             // 1: this layer's output is a later layer's residual: hold it
+};
+
+struct ChainArgs {
+    int H, W, L;
+    int PW, PL, ZO;
+    int res0;             // 1: x itself is a later layer's residual: hold it
+    ChainLayer layer[kChainMax];
+};
+
+// Exact 3-way split of 4 fp32 values (split3 of po2q_x3_dev.h, 4 lanes of it): 4 bf16 per plane.
+__device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mid, uint2& lo) {
+    uint32_t b[4], mb[4], lb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        b[j] = __float_as_uint(v[j]);
+        const float xc = __builtin_amdgcn_fmed3f(v[j], -3.40282347e38f, 3.40282347e38f);
+        const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
+        mb[j] = __float_as_uint(r1) & 0xffff0000u;
+        lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
+    }
+    hi = make_uint2((b[0] >> 16) | (b[1] & 0xffff0000u), (b[2] >> 16) | (b[3] & 0xffff0000u));
+    mid = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
+    lo = make_uint2((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u));
+}
+
+// C: channels; MG: most 16-pixel groups one wave owns (register arrays).  The activation lives
+// in LDS as split planes for the whole chain: per layer every wave first computes ALL its
+// groups' accumulators (transposed MFMA form, A = weights, B = pixels: each lane ends with 4
+// consecutive output channels of one pixel), a barrier retires every read of the layer's input,
+// then the epilogue overwrites the planes in place (ds_write_b64 of 4 bf16 per plane) -- or, in
+// the last layer, stores y.  A residual source (a BasicBlock's input) is held in VGPRs by the
+// lanes that will add it: every layer maps (wave, lane) to the same (pixel, channels).
+template <int C, int MG>
+__global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __restrict__ x, float* __restrict__ y,
+                                                               ChainArgs a) {
+    constexpr int KS = C == 16 ? 2 : 3 * (C / 32);  // k-steps per tap row
+    constexpr int NO = C / 8;                       // channel octets per pixel
+    constexpr int NT = C / 16;                      // output tiles
+    constexpr int WPT = (kChainThreads / 64) / NT;  // waves per output tile
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n = blockIdx.x;
+    const int nt = wave % NT, gsub = wave / NT;
+    const int H = a.H, W = a.W, PW = a.PW, HW = H * W;
+    const int ngroups = (HW + 15) >> 4;
+    const int p = lane & 15, g4 = lane >> 4;
+    const int c0 = 16 * nt + 4 * g4;  // this lane's 4 output channels (transposed form)
+    const int64_t img = (int64_t)C * HW;
+    const float* xn = x + (int64_t)n * img;
+    float* yn = y + (int64_t)n * img;
+
+    // ---- x -> split planes, the zero halo with it (written once: later layers write interiors)
+    const int nitems = (H + 2) * PW * NO;
+    for (int base = 0; base < nitems; base += kChainThreads * kChainItems) {
+        uint32_t v[kChainItems][8];
+        int dst[kChainItems];
+#pragma unroll
+        for (int i = 0; i < kChainItems; ++i) {
+            const int it = base + i * kChainThreads + tid;
+            const bool ok = it < nitems;
+            const int pc = it % PW, t = it / PW;
+            const int rr = t % (H + 2), oc = t / (H + 2);
+            const int h = rr - 1, xc = pc - 1;
+            const bool inb = ok && h >= 0 && h < H && xc >= 0 && xc < W;
+            const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
+            dst[i] = ok ? ch_addr<C>(rr * PW + pc, oc) : -1;
+        }
+#pragma unroll
+        for (int i = 0; i < kChainItems; ++i) {
+            if (dst[i] < 0) continue;
+            uint4 hi, mid, lo;
+            split3(v[i], hi, mid, lo);
+            *reinterpret_cast<uint4*>(lds + dst[i]) = hi;
+            *reinterpret_cast<uint4*>(lds + a.PL + dst[i]) = mid;
+            *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst[i]) = lo;
+        }
+    }
+    if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.PL + a.ZO) = make_uint4(0u, 0u, 0u, 0u);
+    // the held residual: x itself when a later layer adds it
+    float rres[MG][4];
+#pragma unroll
+    for (int gi = 0; gi < MG; ++gi) {
+        const int f = 16 * (gsub + gi * WPT) + p;
+        const bool ok = a.res0 && f < HW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rres[gi][i] = ok ? xn[(int64_t)(c0 + i) * HW + f] : 0.0f;
+    }
+    __syncthreads();
+
+    // this wave's groups: padded pixel of tap (0, 0) per group (past the image: pixel 0, the
+    // result is not stored -- every group runs the same unrolled MFMA sequence)
+    int pp0[MG];
+#pragma unroll
+    for (int gi = 0; gi < MG; ++gi) {
+        const int grp = gsub + gi * WPT;
+        const int f = 16 * grp + p;
+        const int fo = (grp < ngroups && f < HW) ? f : 0;
+        const int oy = fo / W;
+        pp0[gi] = oy * PW + fo - oy * W;
+    }
+    // A-fragment (pixel) address of step st = (group, tap row r, k-step ks) in a plane
+    auto a_addr = [&](auto ST_) __attribute__((always_inline)) {
+        constexpr int st = decltype(ST_)::value;
+        constexpr int gi = st / (3 * KS), t = st % (3 * KS), r = t / KS, ks = t % KS;
+        if constexpr (C == 16) {
+            const int s = ks == 0 ? (g4 >> 1) : 2;
+            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C>(pp0[gi] + r * PW + s, g4 & 1);
+        } else {
+            return ch_addr<C>(pp0[gi] + r * PW + ks % 3, (ks / 3) * 4 + g4);
+        }
+    };
+    constexpr int T = 3 * KS;    // MFMA steps (x 3 planes) per group
+    constexpr int S = MG * T;    // steps per layer
+    constexpr int PD = 4;        // A-fragment reads issued this many steps ahead (3 each: lgkmcnt <= 12)
+
+    // the first layer's B fragments and epilogue constants (later layers': prefetched in the
+    // previous layer, behind its MFMAs)
+    bf16x8 bw[3 * KS];
+    float bk[4], eps_[4], epb_[4];
+    auto load_layer = [&](const ChainLayer& ly) __attribute__((always_inline)) {
+#pragma unroll
+        for (int f = 0; f < 3 * KS; ++f) bw[f] = __builtin_bit_cast(bf16x8, ly.wp[(f * NT + nt) * 64 + lane]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bk[i] = ly.bias ? ly.bias[c0 + i] : 0.0f;
+            eps_[i] = ly.ps ? ly.ps[c0 + i] : 1.0f;
+            epb_[i] = ly.pb ? ly.pb[c0 + i] : 0.0f;
+        }
+    };
+    load_layer(a.layer[0]);
+
+    for (int l = 0; l < a.L; ++l) {
+        const ChainLayer& ly = a.layer[l];
+        // opaque per layer: keeps the step addresses from being hoisted out of the layer loop
+        // (one VGPR per step held across every layer)
+#pragma unroll
+        for (int gi = 0; gi < MG; ++gi) asm volatile("" : "+v"(pp0[gi]));
+        // ---- every group's accumulator (the planes are read-only in this phase), software-
+        // pipelined: the 3 plane reads of step st + PD go out before the MFMAs of step st
+        floatx4 acc[MG];
+#pragma unroll
+        for (int gi = 0; gi < MG; ++gi) acc[gi] = floatx4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 ring[PD + 1][3];
+        auto issue = [&](auto ST_) __attribute__((always_inline)) {
+            constexpr int st = decltype(ST_)::value;
+            if constexpr (st < S) {
+                const int ad = a_addr(ST_);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    ring[st % (PD + 1)][pl] =
+                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + pl * a.PL + ad));
+            }
+        };
+        auto step = [&](auto ST_) __attribute__((always_inline)) {
+            constexpr int st = decltype(ST_)::value;
+            issue(std::integral_constant<int, st + PD>{});
+            constexpr int gi = st / T, t = st % T;
+            const bf16x8 bb = bw[t];  // t = r * KS + ks: the pack's fragment order
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)  // transposed: D[out channel][pixel]
+                acc[gi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb, ring[st % (PD + 1)][pl], acc[gi], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for<PD>(issue);
+        static_for<S>(step);
+
+        // this layer's epilogue constants; the next layer's B fragments / constants go out now
+        const float scale = *ly.scale;
+        const bool last = l + 1 == a.L;
+        const int act = ly.act, res_add = ly.res_add, keep = ly.keep;
+        float cbk[4], ceps[4], cepb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cbk[i] = bk[i];
+            ceps[i] = eps_[i];
+            cepb[i] = epb_[i];
+        }
+        if (!last) load_layer(a.layer[l + 1]);
+        __syncthreads();  // every read of this layer's input planes has retired
+
+        // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p
+#pragma unroll
+        for (int gi = 0; gi < MG; ++gi) {
+            const int grp = gsub + gi * WPT;
+            const int f = 16 * grp + p;
+            if (grp >= ngroups || f >= HW) continue;
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float u = (acc[gi][i] * scale + cbk[i]) * ceps[i] + cepb[i];
+                if (res_add) u += rres[gi][i];
+                v[i] = epi_act(u, act);
+                if (keep) rres[gi][i] = v[i];
+            }
+            if (last) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) yn[(int64_t)(c0 + i) * HW + f] = v[i];
+            } else {
+                const int oy = f / W, ox = f - oy * W;
+                const int ad = ch_addr<C>((oy + 1) * PW + ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
+                uint2 hi, mid, lo;
+                split4(v, hi, mid, lo);
+                *reinterpret_cast<uint2*>(lds + ad) = hi;
+                *reinterpret_cast<uint2*>(lds + a.PL + ad) = mid;
+                *reinterpret_cast<uint2*>(lds + 2 * a.PL + ad) = lo;
+            }
+        }
+        __syncthreads();  // the next layer's input planes are complete
+    }
+}
+
+// ------------------------------------------------------------------- host side --
+// most 16-pixel groups one wave owns: ceil(ceil(HW / 16) / waves per output tile); the register
+// arrays take up to 8 (C = 16: 32x32) or 4 (C = 32: 16x16, C = 64: 8x16) without spilling
+static int chain_mg(int64_t C, int64_t H, int64_t W) {
+    const int64_t groups = (H * W + 15) / 16, wpt = (kChainThreads / 64) / (C / 16);
+    return (int)((groups + wpt - 1) / wpt);
+}
+static int chain_mg_max(int64_t C) { return C == 16 ? 8 : 4; }
+
+static bool chain_geom_ok(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers) {
+    if (!(C == 16 || C == 32 || C == 64) || N < 1 || H < 1 || W < 4 || W % 4 != 0) return false;
+    if (n_layers < 1 || n_layers > kChainMax || N > INT32_MAX) return false;
+    if (N * C * H * W >= (1LL << 40) || chain_mg(C, H, W) > chain_mg_max(C)) return false;
+    return 3 * chain_plane(C, H, W) <= kChainLdsMax;
+}
+
+static bool chain_mode_ok(int bits, int fsr, int mode) {
+    if (mode != PO2Q_MODE_PO2 && mode != PO2Q_MODE_PO2_PLUS) return false;
+    if (bits < 1 || bits > 16) return false;
+    const long lo = (long)fsr - (1L << (bits - 1)), hi = (long)fsr - 1;
+    return lo >= -126 && hi <= 127;  // +-2^e must be a normal bf16
+}
+
+// The pack geometry of one layer (the small-image kernel's row layout).
+static ConvPlan chain_plan(int64_t N, int64_t C, int64_t H, int64_t W) {
+    ConvPlan p{};
+    p.N = (int)N; p.C = (int)C; p.H = (int)H; p.W = (int)W; p.K = (int)C;
+    p.R = p.S = 3; p.sh = p.sw = 1; p.ph = p.pw = 1; p.dh = p.dw = 1; p.groups = 1;
+    p.P = p.H; p.Q = p.W; p.Cg = p.C; p.Kg = p.K;
+    p.kind = KIND_BF16X3_IMG;
+    p.CC = C == 16 ? 16 : 32;
+    p.nchunks = (int)C / p.CC;
+    p.steps = C == 16 ? 2 : 3 * p.nchunks;
+    p.NT = (int)C / 16;
+    p.taps = 9;
+    p.packed_floats = (int64_t)3 * p.steps * p.NT * 64 * 4;
+    return p;
+}
+
+namespace {
+constexpr size_t kChainAlign = 256;
+size_t chain_align(size_t v) { return (v + kChainAlign - 1) / kChainAlign * kChainAlign; }
+struct ChainWs {
+    size_t packed_off, packed_bytes, scale_off, total;
+};
+ChainWs chain_ws(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers) {
+    ChainWs L;
+    const ConvPlan p = chain_plan(N, C, H, W);
+    L.packed_bytes = chain_align((size_t)p.packed_floats * 4);
+    L.packed_off = 0;
+    L.scale_off = L.packed_bytes * (size_t)n_layers;
+    L.total = L.scale_off + chain_align((size_t)n_layers * 4);
+    return L;
+}
+}  // namespace
+
+}  // namespace po2q
+
+using namespace po2q;
+
+extern "C" {
+
+int po2q_qconv2d_chain_supported(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers, int bits, int fsr,
+                                 int mode) {
+    return chain_geom_ok(N, C, H, W, n_layers) && chain_mode_ok(bits, fsr, mode) ? 1 : 0;
+}
+
+size_t po2q_qconv2d_chain_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t W, int n_layers) {
+    if (!chain_geom_ok(N, C, H, W, n_layers)) return 0;
+    return chain_ws(N, C, H, W, n_layers).total;
+}
+
+int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* const* bias,
+                           const float* const* post_scale, const float* const* post_shift, const int* act,
+                           const int* res_from, int n_layers, int64_t N, int64_t C, int64_t H, int64_t W, int bits,
+                           int fsr, int mode, float* y, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!chain_geom_ok(N, C, H, W, n_layers)) {
+        set_error("po2q: chain needs C in {16, 32, 64}, W % 4 == 0, 1.." + std::to_string(kChainMax) +
+                  " layers and a small image: its split planes in LDS ((H + 2)(W + 2) 6C bytes <= 160 KiB) and "
+                  "at most 8 (C = 16) / 4 (C = 32, 64) 16-pixel groups per wave");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!chain_mode_ok(bits, fsr, mode)) {
+        set_error("po2q: chain needs mode po2 / po2+ with exponents in the bf16 range");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!x || !w || !y || !workspace) {
+        set_error("po2q: chain: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    const ChainWs L = chain_ws(N, C, H, W, n_layers);
+    if (workspace_bytes < L.total) {
+        set_error("po2q: chain workspace too small (need " + std::to_string(L.total) + " bytes)");
+        return PO2Q_ERR_WORKSPACE;
+    }
+    for (int l = 0; l < n_layers; ++l) {
+        if (!w[l]) {
+            set_error("po2q: chain: null weight of layer " + std::to_string(l));
+            return PO2Q_ERR_INVALID;
+        }
+        const int ac = act ? act[l] : 0;
+        if (ac < 0 || ac > 3) {
+            set_error("po2q: chain: unknown activation of layer " + std::to_string(l));
+            return PO2Q_ERR_INVALID;
+        }
+        const int r = res_from ? res_from[l] : -1;
+        if (r < -1 || r > l) {
+            set_error("po2q: chain: res_from[" + std::to_string(l) + "] must be -1 or a layer index <= " +
+                      std::to_string(l) + " (the residual is that layer's input)");
+            return PO2Q_ERR_INVALID;
+        }
+    }
+    // residual sources are held in VGPRs, one at a time: the intervals [source, user] of two
+    // different sources must not overlap (a BasicBlock chain: [2b, 2b + 1] per block)
+    for (int l1 = 0; l1 < n_layers; ++l1)
+        for (int l2 = l1 + 1; l2 < n_layers; ++l2) {
+            const int r1 = res_from ? res_from[l1] : -1, r2 = res_from ? res_from[l2] : -1;
+            if (r1 >= 0 && r2 >= 0 && r1 != r2 && r2 <= l1) {
+                set_error("po2q: chain: res_from holds one residual source at a time (layers " + std::to_string(l1) +
+                          " and " + std::to_string(l2) + " add different, overlapping sources)");
+                return PO2Q_ERR_INVALID;
+            }
+        }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    char* ws = reinterpret_cast<char*>(workspace);
+
+    // every layer's weight: quantize + pack in ceil(n / 24) launches
+    const ConvPlan plan = chain_plan(N, C, H, W);
+    std::vector<const ConvPlan*> plans((size_t)n_layers, &plan);
+    std::vector<uint16_t*> packed((size_t)n_layers);
+    std::vector<float*> scales((size_t)n_layers);
+    for (int l = 0; l < n_layers; ++l) {
+        packed[l] = reinterpret_cast<uint16_t*>(ws + L.packed_off + (size_t)l * L.packed_bytes);
+        scales[l] = reinterpret_cast<float*>(ws + L.scale_off) + l;
+    }
+    hipError_t he = launch_pack_bf16x3_batch(n_layers, plans.data(), w, packed.data(), scales.data(), bits, fsr,
+                                             mode, s);
+    if (he != hipSuccess) {
+        set_error(std::string("po2q: chain weight pack launch: ") + hipGetErrorString(he));
+        return PO2Q_ERR_HIP;
+    }
+
+    std::vector<int> used((size_t)n_layers + 1, 0);  // input of layer j is a residual source
+    for (int l = 0; l < n_layers; ++l)
+        if (res_from && res_from[l] >= 0) used[res_from[l]] = 1;
+    ChainArgs a{};
+    a.H = (int)H; a.W = (int)W; a.L = n_layers;
+    a.PW = (int)W + 2;
+    a.PL = (int)chain_plane(C, H, W);
+    a.ZO = a.PL - 16;
+    a.res0 = used[0];
+    for (int l = 0; l < n_layers; ++l) {
+        ChainLayer& ly = a.layer[l];
+        ly.wp = reinterpret_cast<const uint4*>(packed[l]);
+        ly.scale = scales[l];
+        ly.bias = bias ? bias[l] : nullptr;
+        ly.ps = post_scale ? post_scale[l] : nullptr;
+        ly.pb = post_shift ? post_shift[l] : nullptr;
+        ly.act = act ? act[l] : 0;
+        ly.res_add = (res_from && res_from[l] >= 0) ? 1 : 0;
+        ly.keep = used[l + 1];
+    }
+    const size_t lds = 3 * (size_t)a.PL;
+    const dim3 grid((unsigned)N), block(kChainThreads);
+    const int mg = chain_mg(C, H, W);
+#define PO2Q_CH(c, m)                                                                  \
+    if (C == c && mg <= m) {                                                           \
+        hipLaunchKernelGGL((conv_chain<c, m>), grid, block, lds, s, x, y, a);         \
+    } else
+    PO2Q_CH(16, 2) PO2Q_CH(16, 4) PO2Q_CH(16, 8)
+    PO2Q_CH(32, 2) PO2Q_CH(32, 4)
+    PO2Q_CH(64, 2) PO2Q_CH(64, 4) {
+        set_error("po2q: chain: no kernel for this shape");
+        return PO2Q_ERR_INVALID;
+    }
+#undef PO2Q_CH
+    he = hipGetLastError();
+    if (he != hipSuccess) {
+        set_error(std::string("po2q: chain launch: ") + hipGetErrorString(he));
+        return PO2Q_ERR_HIP;
+    }
+    return PO2Q_OK;
+}
+
+}  // extern "C"

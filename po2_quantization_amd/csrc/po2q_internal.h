@@ -153,7 +153,7 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
                               int bits, int fsr, int mode, uint16_t* packed, float* scale_out,
                               hipStream_t s);
 
-// The same for n weight tensors (plans[i] bf16x3 kinds, fused absmax) in ceil(n / 16) launches.
+// The same for n weight tensors (plans[i] bf16x3 kinds, fused absmax) in ceil(n / 24) launches.
 hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
                                     uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
                                     hipStream_t s);

@@ -295,7 +295,7 @@ struct PackJob {
     int lo, hi, mode, nb;
     PackX3 pg;
 };
-constexpr int kPackBatch = 16;
+constexpr int kPackBatch = 24;  // 24 x 96-byte jobs: 2.3 KB of kernel arguments
 struct PackBatch {
     PackJob job[kPackBatch];
 };

@@ -148,8 +148,63 @@ class ResNet(nn.Module):
             x = plain_conv_fused(self.conv1, x, bn=self.bn1, act="relu")
         else:
             x = self.relu(self.bn1(self.conv1(x)))
-        x = self.layer3(self.layer2(self.layer1(x)))
+        for layer in (self.layer1, self.layer2, self.layer3):
+            x = self._stage(layer, x)
         return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def _stage(self, layer, x):
+        """One residual stage (resnet.py:131-143 builds it).  In inference at small image sizes the
+        stage's identity-shortcut blocks run as ONE chain launch (po2q_qconv2d_chain_f32: every
+        block's conv1 -> bn1 -> relu -> conv2 -> bn2 -> + block input -> relu, one GPU block per
+        image); its first block, when it carries the projection shortcut, runs on its own first."""
+        blocks = list(layer)
+        i0 = 1 if blocks and isinstance(blocks[0], BasicBlock) and blocks[0].downsample is not None else 0
+        run = blocks[i0:]
+        if not run or not self._chain_ok(run, x if i0 == 0 else None):
+            return layer(x)
+        if i0:
+            x = blocks[0](x)
+        if not self._chain_ok(run, x):
+            for b in run:
+                x = b(x)
+            return x
+        ws, bs, ps, pb, res = [], [], [], [], []
+        for b in run:
+            p1, s1 = fold_bn(b.bn1)
+            p2, s2 = fold_bn(b.bn2)
+            res += [-1, len(ws)]  # conv2's shortcut: the block input = conv1's input
+            ws += [b.conv1.weight, b.conv2.weight]
+            bs += [b.conv1.bias, b.conv2.bias]
+            ps += [p1, p2]
+            pb += [s1, s2]
+        c = run[0].conv1
+        return _lib.qconv2d_chain(x, ws, c.bits, NATIVE_MODES[c.quantize_fn], biases=bs, post_scales=ps,
+                                  post_shifts=pb, acts=["relu"] * len(ws), res_from=res)
+
+    @staticmethod
+    def _chain_ok(run, x):
+        """Every block a BasicBlock with an identity shortcut, eval BatchNorms, 3x3 / stride-1 C -> C
+        convs with the same native PO2 quantizer and bits; with x: the chain kernel takes the shape."""
+        c0 = run[0].conv1 if isinstance(run[0], BasicBlock) else None
+        if c0 is None:
+            return False
+        mode = NATIVE_MODES.get(c0.quantize_fn)
+        if mode not in ("po2", "po2+") or c0.precision == "fp32":
+            return False
+        for b in run:
+            if not isinstance(b, BasicBlock) or b.downsample is not None or not can_fuse(b.bn1, b.bn2):
+                return False
+            for c in (b.conv1, b.conv2):
+                if not (isinstance(c, QuantizedConv2d) and c.quantize_fn is c0.quantize_fn and c.bits == c0.bits
+                        and c.precision == c0.precision and tuple(c.kernel_size) == (3, 3)
+                        and tuple(c.stride) == (1, 1) and tuple(c.padding) == (1, 1) and tuple(c.dilation) == (1, 1)
+                        and c.groups == 1 and c.padding_mode == "zeros" and c.in_channels == c0.in_channels
+                        and c.out_channels == c0.in_channels):
+                    return False
+        if x is None:
+            return True
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == c0.in_channels
+                and _lib.chain_supported(x.shape, 2 * len(run), c0.bits, NATIVE_MODES[c0.quantize_fn]))
 
     def get_quantization_error(self):
         """(sum of squared quantization error, element count) over the residual stages.

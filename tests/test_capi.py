@@ -152,3 +152,20 @@ def test_small_image_plans_on_host():
         assert len(set(ps)) == len(ps)
     assert not any("bf16x3_img" in p for p in _lib.plans(256, 16, 224, 224, 16, 3, 3, 1, 1))
     assert not any("bf16x3_img" in p for p in _lib.plans(2, 16, 10, 10, 16, 3, 3, 1, 1))  # W % 4 != 0
+
+
+def test_chain_eligibility_on_host():
+    """po2q_qconv2d_chain: CIFAR-size stride-1 runs (C in {16, 32, 64}, the padded image's split
+    planes in LDS), po2 / po2+ only; the workspace holds every layer's pack."""
+    assert _lib.chain_supported((256, 16, 32, 32), 18) and _lib.chain_supported((256, 32, 16, 16), 17)
+    assert _lib.chain_supported((256, 64, 8, 8), 17, mode="po2+")
+    assert not _lib.chain_supported((256, 16, 224, 224), 18)          # planes exceed LDS
+    assert not _lib.chain_supported((256, 48, 8, 8), 4)               # channel count
+    assert not _lib.chain_supported((256, 16, 32, 30), 4)             # W % 4
+    assert not _lib.chain_supported((256, 16, 32, 32), 25)            # PO2Q_CHAIN_MAX_LAYERS
+    assert not _lib.chain_supported((256, 16, 32, 32), 4, mode="none")
+    L = _lib.load()
+    n = L.po2q_qconv2d_chain_workspace_bytes(256, 16, 32, 32, 18)
+    assert 18 * 3 * 2 * 64 * 16 <= n < 1 << 20  # the packs and scales: activations stay in LDS
+    assert not _lib.chain_supported((256, 64, 16, 16), 4)           # more pixel groups than a wave holds
+    assert L.po2q_qconv2d_chain_workspace_bytes(256, 16, 224, 224, 18) == 0

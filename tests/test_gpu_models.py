@@ -44,6 +44,30 @@ def test_qat_mode_logits(spec, q, bits):
     assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
 
 
+@pytest.mark.parametrize("spec,q,bits,n", [("resnet56", "po2", 4, 9), ("resnet20", "po2+", 3, 3)])
+def test_cifar_resnet_logits_through_chain_kernel(spec, q, bits, n, monkeypatch):
+    """At CIFAR size the eval forward runs each stage's identity-shortcut blocks as ONE chain launch
+    (po2q_qconv2d_chain_f32: stage 1 all n blocks, stages 2-3 the n - 1 after the transition); the
+    logits still match the reference's (reference resnet.py:55-71, 190-201)."""
+    from po2_quantization_amd import _lib
+
+    calls = []
+    orig = _lib.qconv2d_chain
+
+    def counted(x, ws, *a, **k):
+        calls.append(len(ws))
+        return orig(x, ws, *a, **k)
+
+    monkeypatch.setattr(_lib, "qconv2d_chain", counted)
+    d = load_npz("models.npz")
+    m = build(spec, q, bits)
+    with torch.no_grad():
+        y = m(torch.from_numpy(d["x/cifar8"]).to(DEV)).cpu().numpy()
+    assert calls == [2 * n, 2 * (n - 1), 2 * (n - 1)], calls
+    ref = d["logits/%s/%s/%d" % (spec, q, bits)]
+    assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
+
+
 @pytest.mark.parametrize("qn", ["po2", "po2+", "lin", "lin+"])
 def test_ptq_config1_resnet20(qn):
     """Config 1 (test.py PTQ path): quantize_model(model, quantizer, 4) then eval."""

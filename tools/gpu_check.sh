@@ -54,6 +54,9 @@ for s in $STEPS; do
                if ! grep -q " passed" gpurun_out/dwtests.log || grep -q "failed\|error" gpurun_out/dwtests.log; then
                    echo "stopping: depthwise GPU tests did not pass"; exit 1
                fi ;;
+        chaintests) run chaintests 600 python -u -m pytest tests/test_gpu_chain.py -m gpu -x -q --timeout 300 --timeout-method thread
+               if ! grep -q " passed" gpurun_out/chaintests.log || grep -q "failed\|error" gpurun_out/chaintests.log; then
+                   echo "stopping: chain tests failed"; exit 3; fi ;;
         c64res) run c64res 600 python -u -m pytest tests/test_gpu_conv.py -m gpu -x -q --timeout 300 --timeout-method thread -k "c64_residual or fused_epilogue"
                if ! grep -q " passed" gpurun_out/c64res.log || grep -q "failed\|error" gpurun_out/c64res.log; then
                    echo "stopping: c64res failed"; exit 3; fi ;;
@@ -90,6 +93,8 @@ for s in $STEPS; do
         bench32) run bench32 600 python bench.py --image 32 --steps 20 --warmup 3 --no-cpu-baseline ;;
         bench32g) run bench32g 600 python bench.py --image 32 --steps 50 --warmup 3 --graph --no-cpu-baseline ;;
         sweep) run sweep 900 python tools/tile_sweep.py ;;
+        profc2) run profc2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2 -o run \
+                  -- python bench.py --image 32 --steps 50 --warmup 3 --graph --no-cpu-baseline --no-cifar --no-models ;;
         sweepc) run sweepc 600 python tools/tile_sweep.py --shapes 7,8,9 --iters 21 ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep1) run sweep1 600 python tools/tile_sweep.py --shapes 1 --iters 21 ;;
@@ -100,6 +105,11 @@ for s in $STEPS; do
         pmc1) run pmc1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1 --tile 7,4,112" s1 ;;
         pmcs3) run pmcs3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" s3 "conv_rowsk" all
                python3 tools/pmc_summary.py gpurun_out/pmc_s3 177.6 > gpurun_out/pmc_s3_summary.txt 2>&1 ;;
+        pmcch) for st in 1 3; do  # useful bf16 MFMA GFLOP per launch: 18 (17) layers x 3 x 1.208
+                   gf=$([ $st = 1 ] && echo 65.2 || echo 61.6)
+                   run pmcch$st 600 env PMC_DRIVER=tools/prof_chain.py bash tools/pmc.sh "--stage $st" ch$st "conv_chain" all
+                   python3 tools/pmc_summary.py gpurun_out/pmc_ch$st $gf > gpurun_out/pmc_ch${st}_summary.txt 2>&1
+               done ;;
         pmcs2) run pmcs2 900 bash tools/pmc.sh "--shape 32,112,32,3,1,1" s2 "conv_rowsf" all
                python3 tools/pmc_summary.py gpurun_out/pmc_s2 177.6 > gpurun_out/pmc_s2_summary.txt 2>&1 ;;
         pmc3) run pmc3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1 --tile 4,8,32" s3 ;;

@@ -24,7 +24,7 @@ i=0
 for g in "${GROUPS_[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-include-regex "$KRE" --pmc $g --output-format csv -d "$OUT/g$i" -o run \
-      -- python3 tools/prof_layer.py $ARGS > "$OUT/g$i.log" 2>&1
+      -- python3 "${PMC_DRIVER:-tools/prof_layer.py}" $ARGS > "$OUT/g$i.log" 2>&1
   rc=$?
   echo "pmc group $i rc=$rc: $g" | tee -a "$OUT/status.txt"
   if [ $rc -ge 124 ]; then echo "stopping (rc=$rc)"; exit $rc; fi
