@@ -6,8 +6,9 @@
 // Why: at 32x32 / 16x16 / 8x8 a layer is 4-17 MB and its arithmetic a microsecond or two of
 // MFMA time per CU, so one launch per layer spends most of its ~10 us in the launch, the first
 // load's latency, the store drain -- and, even in one launch, in the global round trip of every
-// activation (profiles/r03_cifar32_kernel_stats.csv).  Images are independent through the whole
-// stage, so a block owns ONE image for every layer, and the activation never leaves the CU:
+// activation (profiles/r03_cifar32_chain_kernel_stats.csv: the single-layer autotune
+// candidates).  Images are independent through the whole stage, so a block owns ONE image for
+// every layer, and the activation never leaves the CU:
 //   start:      x -> exact hi / mid / lo bf16 split planes [(H + 2) x (W + 2) padded pixels][C]
 //               in LDS (zero halo), one batch of independent loads per thread;
 //   per layer:  every wave computes ALL its 16-pixel groups' accumulators for its 16-channel
@@ -44,14 +45,16 @@ constexpr int kChainItems = 5;      // split items (pixel x channel octet) per t
 constexpr int kChainMax = PO2Q_CHAIN_MAX_LAYERS;
 constexpr size_t kChainLdsMax = 160 * 1024;
 
+// Byte offset of channel octet oc of padded pixel pp in a plane: the conflict-free swizzle of
+// po2q_conv_img.hip (every ds_read_b128 lane group of a fragment read hits 64 distinct banks).
 template <int C>
 __device__ __forceinline__ int ch_addr(int pp, int oc) {
     if constexpr (C == 16)
-        return pp * 32 + 16 * (oc ^ ((pp >> 3) & 1));
+        return pp * 32 + 16 * oc;
     else if constexpr (C == 32)
-        return pp * 64 + 16 * (oc ^ ((pp >> 2) & 3));
+        return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
     else
-        return pp * 128 + 16 * (oc ^ ((pp >> 1) & 7));
+        return pp * 128 + 16 * (oc ^ (((pp >> 1) & 3) << 1));
 }
 
 size_t chain_plane(int64_t C, int64_t H, int64_t W) { return (size_t)((H + 2) * (W + 2) * 2 * C + 16); }
