@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -45,16 +46,23 @@ constexpr int kChainItems = 5;      // split items (pixel x channel octet) per t
 constexpr int kChainMax = PO2Q_CHAIN_MAX_LAYERS;
 constexpr size_t kChainLdsMax = 160 * 1024;
 
-// Byte offset of channel octet oc of padded pixel pp in a plane: the conflict-free swizzle of
-// po2q_conv_img.hip (every ds_read_b128 lane group of a fragment read hits 64 distinct banks).
-template <int C>
-__device__ __forceinline__ int ch_addr(int pp, int oc) {
-    if constexpr (C == 16)
-        return pp * 32 + 16 * oc;
-    else if constexpr (C == 32)
+// Byte offset of channel octet oc of padded pixel pp (padded column col) in a plane: the
+// conflict-free swizzle of po2q_conv_img.hip (every ds_read_b128 lane group of a fragment read
+// hits 64 distinct banks when a 16-pixel group is 16 consecutive pixels).  W8 (C = 64, W = 8: a
+// group is two 8-pixel row pieces 10 padded pixels apart): the octet XORed with a per-column
+// table instead (exhaustive search over every tap offset, tools-free: 3 bits per column).
+template <int C, bool W8 = false, bool S16 = true>
+__device__ __forceinline__ int ch_addr(int pp, int col, int oc) {
+    if constexpr (C == 16) {
+        // S16: the octet flipped with pixel bit 2 also halves the epilogue ds_write_b64 conflicts
+        return pp * 32 + 16 * (S16 ? (oc ^ ((pp >> 2) & 1)) : oc);
+    } else if constexpr (C == 32) {
         return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
-    else
+    } else if constexpr (W8) {
+        return pp * 128 + 16 * (oc ^ (int)((0x53e0e1u >> (3 * (col & 7))) & 7u));
+    } else {
         return pp * 128 + 16 * (oc ^ (((pp >> 1) & 3) << 1));
+    }
 }
 
 size_t chain_plane(int64_t C, int64_t H, int64_t W) { return (size_t)((H + 2) * (W + 2) * 2 * C + 16); }
@@ -111,7 +119,9 @@ __device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mi
 // then the epilogue overwrites the planes in place (ds_write_b64 of 4 bf16 per plane) -- or, in
 // the last layer, stores y.  A residual source (a BasicBlock's input) is held in VGPRs by the
 // lanes that will add it: every layer maps (wave, lane) to the same (pixel, channels).
-template <int C, int MG>
+// FULL: every wave owns exactly MG whole groups (H * W a multiple of 16 * waves per tile * MG):
+// no per-group bounds checks (the CIFAR stages).
+template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = true>
 __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __restrict__ x, float* __restrict__ y,
                                                                ChainArgs a) {
     constexpr int KS = C == 16 ? 2 : 3 * (C / 32);  // k-steps per tap row
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
-            dst[i] = ok ? ch_addr<C>(rr * PW + pc, oc) : -1;
+            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc) : -1;
         }
 #pragma unroll
         for (int i = 0; i < kChainItems; ++i) {
@@ -173,14 +183,15 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
 
     // this wave's groups: padded pixel of tap (0, 0) per group (past the image: pixel 0, the
     // result is not stored -- every group runs the same unrolled MFMA sequence)
-    int pp0[MG];
+    int pp0[MG], px0[MG];
 #pragma unroll
     for (int gi = 0; gi < MG; ++gi) {
         const int grp = gsub + gi * WPT;
         const int f = 16 * grp + p;
-        const int fo = (grp < ngroups && f < HW) ? f : 0;
+        const int fo = (FULL || (grp < ngroups && f < HW)) ? f : 0;
         const int oy = fo / W;
-        pp0[gi] = oy * PW + fo - oy * W;
+        px0[gi] = fo - oy * W;
+        pp0[gi] = oy * PW + px0[gi];
     }
     // A-fragment (pixel) address of step st = (group, tap row r, k-step ks) in a plane
     auto a_addr = [&](auto ST_) __attribute__((always_inline)) {
@@ -188,37 +199,39 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         constexpr int gi = st / (3 * KS), t = st % (3 * KS), r = t / KS, ks = t % KS;
         if constexpr (C == 16) {
             const int s = ks == 0 ? (g4 >> 1) : 2;
-            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C>(pp0[gi] + r * PW + s, g4 & 1);
+            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1);
         } else {
-            return ch_addr<C>(pp0[gi] + r * PW + ks % 3, (ks / 3) * 4 + g4);
+            return ch_addr<C, W8, S16>(pp0[gi] + r * PW + ks % 3, px0[gi] + ks % 3, (ks / 3) * 4 + g4);
         }
     };
     constexpr int T = 3 * KS;    // MFMA steps (x 3 planes) per group
     constexpr int S = MG * T;    // steps per layer
     constexpr int PD = 4;        // A-fragment reads issued this many steps ahead (3 each: lgkmcnt <= 12)
 
-    // the first layer's B fragments and epilogue constants (later layers': prefetched in the
-    // previous layer, behind its MFMAs)
+    // the first layer's B fragments (later layers': prefetched behind the previous layer's MFMAs,
+    // straight into the registers the next MFMAs read -- no loop-carried copy to wait for)
     bf16x8 bw[3 * KS];
-    float bk[4], eps_[4], epb_[4];
-    auto load_layer = [&](const ChainLayer& ly) __attribute__((always_inline)) {
+    auto load_bw = [&](const ChainLayer& ly) __attribute__((always_inline)) {
 #pragma unroll
         for (int f = 0; f < 3 * KS; ++f) bw[f] = __builtin_bit_cast(bf16x8, ly.wp[(f * NT + nt) * 64 + lane]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            bk[i] = ly.bias ? ly.bias[c0 + i] : 0.0f;
-            eps_[i] = ly.ps ? ly.ps[c0 + i] : 1.0f;
-            epb_[i] = ly.pb ? ly.pb[c0 + i] : 0.0f;
-        }
     };
-    load_layer(a.layer[0]);
+    load_bw(a.layer[0]);
 
     for (int l = 0; l < a.L; ++l) {
         const ChainLayer& ly = a.layer[l];
+        // this layer's epilogue constants: loaded now, consumed after the MFMA phase
+        const float scale = *ly.scale;
+        float cbk[4], ceps[4], cepb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cbk[i] = ly.bias ? ly.bias[c0 + i] : 0.0f;
+            ceps[i] = ly.ps ? ly.ps[c0 + i] : 1.0f;
+            cepb[i] = ly.pb ? ly.pb[c0 + i] : 0.0f;
+        }
         // opaque per layer: keeps the step addresses from being hoisted out of the layer loop
         // (one VGPR per step held across every layer)
 #pragma unroll
-        for (int gi = 0; gi < MG; ++gi) asm volatile("" : "+v"(pp0[gi]));
+        for (int gi = 0; gi < MG; ++gi) asm volatile("" : "+v"(pp0[gi]), "+v"(px0[gi]));
         // ---- every group's accumulator (the planes are read-only in this phase), software-
         // pipelined: the 3 plane reads of step st + PD go out before the MFMAs of step st
         floatx4 acc[MG];
@@ -248,26 +261,22 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         static_for<PD>(issue);
         static_for<S>(step);
 
-        // this layer's epilogue constants; the next layer's B fragments / constants go out now
-        const float scale = *ly.scale;
+        // the next layer's B fragments go out now (the last layer reloads its own: no branch, so
+        // the epilogue's wait for this layer's constants stays a counted vmcnt, not vmcnt(0))
         const bool last = l + 1 == a.L;
         const int act = ly.act, res_add = ly.res_add, keep = ly.keep;
-        float cbk[4], ceps[4], cepb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            cbk[i] = bk[i];
-            ceps[i] = eps_[i];
-            cepb[i] = epb_[i];
-        }
-        if (!last) load_layer(a.layer[l + 1]);
-        __syncthreads();  // every read of this layer's input planes has retired
+        load_bw(a.layer[last ? l : l + 1]);
+        // every read of this layer's input planes has retired.  A bare s_barrier, not
+        // __syncthreads: its release fence would wait for the prefetches just issued (vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
 
         // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p
 #pragma unroll
         for (int gi = 0; gi < MG; ++gi) {
             const int grp = gsub + gi * WPT;
             const int f = 16 * grp + p;
-            if (grp >= ngroups || f >= HW) continue;
+            if (!FULL && (grp >= ngroups || f >= HW)) continue;
             float v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 for (int i = 0; i < 4; ++i) yn[(int64_t)(c0 + i) * HW + f] = v[i];
             } else {
                 const int oy = f / W, ox = f - oy * W;
-                const int ad = ch_addr<C>((oy + 1) * PW + ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
+                const int ad = ch_addr<C, W8, S16>((oy + 1) * PW + ox + 1, ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
                 uint2 hi, mid, lo;
                 split4(v, hi, mid, lo);
                 *reinterpret_cast<uint2*>(lds + ad) = hi;
@@ -289,7 +298,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 *reinterpret_cast<uint2*>(lds + 2 * a.PL + ad) = lo;
             }
         }
-        __syncthreads();  // the next layer's input planes are complete
+        // the next layer's input planes are complete (the block's own LDS writes: lgkmcnt)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
 }
 
@@ -458,13 +469,29 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     const size_t lds = 3 * (size_t)a.PL;
     const dim3 grid((unsigned)N), block(kChainThreads);
     const int mg = chain_mg(C, H, W);
-#define PO2Q_CH(c, m)                                                                  \
-    if (C == c && mg <= m) {                                                           \
-        hipLaunchKernelGGL((conv_chain<c, m>), grid, block, lds, s, x, y, a);         \
+    const bool w8 = C == 64 && W == 8;
+    const int64_t wpt = (kChainThreads / 64) / (C / 16);
+    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes unswizzled
+    const char* venv = getenv("PO2Q_CHAIN_VARIANT");
+    const int variant = venv ? atoi(venv) : 0;
+    const bool full = !(variant & 1) && (H * W) % 16 == 0 && (H * W / 16) % wpt == 0;
+    // the exact-fit forms (FULL) for the CIFAR stages, the checked forms for everything else
+#define PO2Q_CH(c, m, w)                                                                               \
+    if (C == c && mg <= m && w8 == w) {                                                                \
+        if (c == 16 && (variant & 2)) {                                                                \
+            if (full && mg == m)                                                                       \
+                hipLaunchKernelGGL((conv_chain<c, m, w, true, false>), grid, block, lds, s, x, y, a);  \
+            else                                                                                       \
+                hipLaunchKernelGGL((conv_chain<c, m, w, false, false>), grid, block, lds, s, x, y, a); \
+        } else if (full && mg == m) {                                                                  \
+            hipLaunchKernelGGL((conv_chain<c, m, w, true>), grid, block, lds, s, x, y, a);            \
+        } else {                                                                                       \
+            hipLaunchKernelGGL((conv_chain<c, m, w, false>), grid, block, lds, s, x, y, a);           \
+        }                                                                                              \
     } else
-    PO2Q_CH(16, 2) PO2Q_CH(16, 4) PO2Q_CH(16, 8)
-    PO2Q_CH(32, 2) PO2Q_CH(32, 4)
-    PO2Q_CH(64, 2) PO2Q_CH(64, 4) {
+    PO2Q_CH(16, 2, false) PO2Q_CH(16, 4, false) PO2Q_CH(16, 8, false)
+    PO2Q_CH(32, 2, false) PO2Q_CH(32, 4, false)
+    PO2Q_CH(64, 2, true) PO2Q_CH(64, 4, true) PO2Q_CH(64, 2, false) PO2Q_CH(64, 4, false) {
         set_error("po2q: chain: no kernel for this shape");
         return PO2Q_ERR_INVALID;
     }

@@ -65,6 +65,7 @@ def _cpu_standins(setattr_=setattr):
              O.cpu_reference_qconv2d(x, w, b, st, pad, d, g, bits, mode))
     setattr_(_lib, "pair_supported", lambda *a, **k: False)
     setattr_(_lib, "s2ds_supported", lambda *a, **k: False)
+    setattr_(_lib, "chain_supported", lambda *a, **k: False)  # the chain kernel: per-layer calls instead
 
 
 def _chain_worker(rank, world, port, out_dir):

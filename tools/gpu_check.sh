@@ -95,6 +95,7 @@ for s in $STEPS; do
         sweep) run sweep 900 python tools/tile_sweep.py ;;
         profc2) run profc2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2 -o run \
                   -- python bench.py --image 32 --steps 50 --warmup 3 --graph --no-cpu-baseline --no-cifar --no-models ;;
+        chainab) run chainab 300 python tools/chain_ab.py ;;
         sweepc) run sweepc 600 python tools/tile_sweep.py --shapes 7,8,9 --iters 21 ;;
         sweep036) run sweep036 600 python tools/tile_sweep.py --shapes 0,3,6 --iters 15 ;;
         sweep1) run sweep1 600 python tools/tile_sweep.py --shapes 1 --iters 21 ;;
