@@ -51,10 +51,12 @@ constexpr size_t kChainLdsMax = 160 * 1024;
 // hits 64 distinct banks when a 16-pixel group is 16 consecutive pixels).  W8 (C = 64, W = 8: a
 // group is two 8-pixel row pieces 10 padded pixels apart): the octet XORed with a per-column
 // table instead (exhaustive search over every tap offset, tools-free: 3 bits per column).
-template <int C, bool W8 = false, bool S16 = true>
+template <int C, bool W8 = false, bool S16 = false>
 __device__ __forceinline__ int ch_addr(int pp, int col, int oc) {
     if constexpr (C == 16) {
-        // S16: the octet flipped with pixel bit 2 also halves the epilogue ds_write_b64 conflicts
+        // S16 (A/B only): the octet flipped with pixel bit 2 -- by the bank model conflict-free
+        // for the reads and half the epilogue ds_write_b64 conflicts, yet 11 % slower measured
+        // (profiles/r03_chain_ab.json), so the product layout stays unswizzled
         return pp * 32 + 16 * (S16 ? (oc ^ ((pp >> 2) & 1)) : oc);
     } else if constexpr (C == 32) {
         return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
@@ -121,7 +123,7 @@ __device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mi
 // lanes that will add it: every layer maps (wave, lane) to the same (pixel, channels).
 // FULL: every wave owns exactly MG whole groups (H * W a multiple of 16 * waves per tile * MG):
 // no per-group bounds checks (the CIFAR stages).
-template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = true>
+template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = false>
 __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __restrict__ x, float* __restrict__ y,
                                                                ChainArgs a) {
     constexpr int KS = C == 16 ? 2 : 3 * (C / 32);  // k-steps per tap row
@@ -471,7 +473,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     const int mg = chain_mg(C, H, W);
     const bool w8 = C == 64 && W == 8;
     const int64_t wpt = (kChainThreads / 64) / (C / 16);
-    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes unswizzled
+    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes swizzled
     const char* venv = getenv("PO2Q_CHAIN_VARIANT");
     const int variant = venv ? atoi(venv) : 0;
     const bool full = !(variant & 1) && (H * W) % 16 == 0 && (H * W / 16) % wpt == 0;
@@ -480,9 +482,9 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     if (C == c && mg <= m && w8 == w) {                                                                \
         if (c == 16 && (variant & 2)) {                                                                \
             if (full && mg == m)                                                                       \
-                hipLaunchKernelGGL((conv_chain<c, m, w, true, false>), grid, block, lds, s, x, y, a);  \
+                hipLaunchKernelGGL((conv_chain<c, m, w, true, true>), grid, block, lds, s, x, y, a);   \
             else                                                                                       \
-                hipLaunchKernelGGL((conv_chain<c, m, w, false, false>), grid, block, lds, s, x, y, a); \
+                hipLaunchKernelGGL((conv_chain<c, m, w, false, true>), grid, block, lds, s, x, y, a);  \
         } else if (full && mg == m) {                                                                  \
             hipLaunchKernelGGL((conv_chain<c, m, w, true>), grid, block, lds, s, x, y, a);            \
         } else {                                                                                       \
