@@ -200,7 +200,12 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
     // A fragment addresses: x planes (wave-private, pixel = strip column + 1) and shared
     // intermediate planes (pixel = column + 1, swizzled octet o): one b128 each
-    int aoff[NG][KS], yoff[NG][KS];
+    // C = 16 pairs the s2 tap of two planes in one k-step: per halo row and group the k-steps are
+    // (s0 | s1) of each plane, (s2 hi | s2 mid) and (s2 lo | zero) -- 5 MFMAs per tap row where
+    // (s2 | zero) per plane took 6 (the 9 16-channel units of a row fill 4.5 k-steps).  Lanes of
+    // k-half 1 (g >= 2) of the paired fragment read the mid plane, so its offset carries the plane:
+    // aoff[grp][1] / yoff[grp][1] = (s2 hi | s2 mid), aoff2 / yoff2 = (s2 lo | zero slot).
+    int aoff[NG][KS], yoff[NG][KS], aoff2[NG], yoff2[NG];
     {
         const int p = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -208,21 +213,24 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
             const int qc = q0 + 16 * grp + p;  // output column
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                int xp, yp, o;
-                bool zero;
-                if constexpr (CC == 16) {  // ks 0: taps (s0 | s1) x 16 ch; ks 1: (s2 | zero)
-                    xp = 16 * grp + p + (ks == 0 ? (g >> 1) : 2);
-                    yp = qc + (ks == 0 ? (g >> 1) : 2);
-                    o = g & 1;
-                    zero = ks == 1 && g >= 2;
+                if constexpr (CC == 16) {  // ks 0: taps (s0 | s1) x 16 ch; ks 1: the paired s2 fragments
+                    const int xp = 16 * grp + p + (ks == 0 ? (g >> 1) : 2);
+                    const int yp = qc + (ks == 0 ? (g >> 1) : 2);
+                    const int o = g & 1;
+                    if (ks == 0) {
+                        aoff[grp][ks] = xa<CC>(xp, o);
+                        yoff[grp][ks] = yoct<CC>(yp, o);
+                    } else {
+                        aoff[grp][ks] = xa<CC>(xp, o) + (g >= 2 ? PL : 0);
+                        yoff[grp][ks] = yoct<CC>(yp, o) + (g >= 2 ? a.YPL : 0);
+                        aoff2[grp] = g >= 2 ? zero_off : xa<CC>(xp, o) + 2 * PL;
+                        yoff2[grp] = g >= 2 ? yzero : yoct<CC>(yp, o) + 2 * a.YPL;
+                    }
                 } else {  // ks = tap s, k = the 32 channels (octet g)
-                    xp = 16 * grp + p + ks;
-                    yp = qc + ks;
-                    o = g;
-                    zero = false;
+                    aoff[grp][ks] = xa<CC>(16 * grp + p + ks, g);
+                    yoff[grp][ks] = yoct<CC>(qc + ks, g);
+                    aoff2[grp] = yoff2[grp] = 0;
                 }
-                aoff[grp][ks] = zero ? zero_off : xa<CC>(xp, o);
-                yoff[grp][ks] = zero ? yzero : yoct<CC>(yp, o);
             }
         }
     }
@@ -257,16 +265,20 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
+            // fragments of this k-step: the 3 planes, or for C = 16's k-step 1 the two paired ones
+            const int np = (CC == 16 && ks == 1) ? 2 : 3;
             bf16x8 af[3][NG];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                 for (int grp = 0; grp < NG; ++grp) {
-                    if constexpr (TR) {
-                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
-                    } else {
-                        af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * a.YPL + yoff[grp][ks]));
-                    }
+                    if (pl >= np) continue;
+                    int off;
+                    if (CC == 16 && ks == 1)
+                        off = pl == 0 ? (TR ? aoff[grp][1] : yoff[grp][1]) : (TR ? aoff2[grp] : yoff2[grp]);
+                    else
+                        off = TR ? pl * PL + aoff[grp][ks] : pl * a.YPL + yoff[grp][ks];
+                    af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + off));
                 }
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr)
@@ -283,10 +295,12 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-                        for (int grp = 0; grp < NG; ++grp)
+                        for (int grp = 0; grp < NG; ++grp) {
+                            if (pl >= np) continue;
                             acc[SL[rr]][grp][nt] =
                                 TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], acc[SL[rr]][grp][nt], 0, 0, 0)
                                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, acc[SL[rr]][grp][nt], 0, 0, 0);
+                        }
                 }
         }
     };
@@ -342,16 +356,17 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
             // channel 8 + (L & 7)'s first half from lane L + 8): 8 lanes x 16 bytes = one full
             // line per channel, where two 64-byte halves from two stores cost partial-line
             // writes (PMC: 1.32x the output bytes with non-temporal stores).
+            // One DPP move per value: the bank mask restricts the row_ror:8 write to the lanes that
+            // take the other half (banks 2-3 = lanes 8-15 for store A, banks 0-1 for store B), the
+            // others keep `old` -- no zero-initialised temporary and no select.
             const bool hi8 = (lane & 8) != 0;
             floatx4 sa, sb;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float r1 = __int_as_float(
-                    __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][NG - 1][e]), 0x128, 0xf, 0xf, false));
-                const float r0 = __int_as_float(
-                    __builtin_amdgcn_update_dpp(0, __float_as_int(vv[0][0][e]), 0x128, 0xf, 0xf, false));
-                sa[e] = hi8 ? r1 : vv[0][0][e];
-                sb[e] = hi8 ? vv[0][NG - 1][e] : r0;
+                sa[e] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(vv[0][0][e]),
+                                                                   __float_as_int(vv[0][NG - 1][e]), 0x128, 0xf, 0xc, false));
+                sb[e] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(vv[0][NG - 1][e]),
+                                                                   __float_as_int(vv[0][0][e]), 0x128, 0xf, 0x3, false));
             }
             const int q = q0 + (hi8 ? 16 : 0) + 4 * g;
             const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
@@ -433,7 +448,6 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
             for (int grp = 0; grp < NG; ++grp) {
                 const int q = q0 + 16 * grp + p;  // lane: pixel q, channels 16 nt + 4 g .. + 3
-                const bool ok = allok || (irow && q < a.W);
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     uint32_t b4[4];
@@ -450,7 +464,12 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                             const int c = nt * 4 + e;
                             t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
                         }
-                        b4[e] = ok ? __float_as_uint(t) : 0u;
+                        b4[e] = __float_as_uint(t);
+                    }
+                    if (!allok) {  // wave-uniform: only rows / strips that leave the image pay the select
+                        const bool ok = irow && q < a.W;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) b4[e] = ok ? b4[e] : 0u;
                     }
                     uint16_t h[4], m[4], l[4];
 #pragma unroll
@@ -486,7 +505,8 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
 #pragma unroll
         for (int f = 0; f < NF; ++f)
-            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr));
+            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr,
+                                                             CC == 16));
         __syncthreads();  // red / thr reads of conv 1 done
         scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
         if constexpr (WL2) {
@@ -494,8 +514,8 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         } else {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
-                bw2[WL2 ? 0 : f] =
-                    __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
+                bw2[WL2 ? 0 : f] = __builtin_bit_cast(
+                    bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr, CC == 16));
         }
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {

@@ -142,8 +142,10 @@ __device__ __forceinline__ unsigned wq_absmax(const float* __restrict__ w, int n
 // B fragment j of the row layout [r][ks][nt][lane][8] (pack_bf16x3_kernel, vr == 2):
 // CC = 16: ks 0 -> k < 16: s = 0, k >= 16: s = 1; ks 1 -> k < 16: s = 2, else 0.
 // CC = 32: ks = chunk * 3 + s, k = the chunk's 32 channels.
+// dup (CC = 16): k-step 1 holds the s2 tap in BOTH halves, (s2 | s2) instead of (s2 | 0), for the
+// kernels that pair the s2 tap of two planes in one k-step (conv_pair: (s2 hi | s2 mid), (s2 lo | 0)).
 __device__ __forceinline__ uint4 wq_frag_rows(const WQuant& q, int C, int K, int CC, int NT, int ksteps, int j,
-                                              float scale, bool fin, const unsigned* thr) {
+                                              float scale, bool fin, const unsigned* thr, bool dup = false) {
     const int lane = j & 63, t = j >> 6;
     const int nt = t % NT;
     const int ks = (t / NT) % ksteps;
@@ -151,7 +153,7 @@ __device__ __forceinline__ uint4 wq_frag_rows(const WQuant& q, int C, int K, int
     const int grp = lane >> 4;
     int sft, c0;
     if (CC == 16) {
-        sft = ks == 0 ? (grp >> 1) : (grp < 2 ? 2 : -1);
+        sft = ks == 0 ? (grp >> 1) : ((grp < 2 || dup) ? 2 : -1);
         c0 = 8 * (grp & 1);
     } else {
         sft = ks % 3;

@@ -284,7 +284,7 @@ at::Tensor dilate(const at::Tensor& x_, at::IntArrayRef stride, at::IntArrayRef 
     return out;
 }
 
-// Two chained 16-channel 3x3 convs in one launch (po2q_qconv2d_pair_f32)
+// Two chained C -> C -> C 3x3 convs (C in {16, 32}) in one launch (po2q_qconv2d_pair_f32)
 void check_vec(const c10::optional<at::Tensor>& t, const at::Tensor& x, int64_t n, const char* what) {
     if (!t.has_value()) return;
     check_hip_f32(*t, what);

@@ -35,6 +35,9 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // +-inf would give r1 = inf - inf = NaN where the reference's product is +-inf, so
 // r1 comes from the value clamped to +-FLT_MAX (v_med3: identity on every finite value):
 // hi keeps +-inf, mid / lo are finite, and the products sum to +-inf as the reference's do.
+// (a >> 16) | (b & 0xffff0000): the bf16 halves of a (low) and b (high) as one dword
+__device__ __forceinline__ uint32_t pk_hi16(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
 __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
     uint32_t mb[8], lb[8];
 #pragma unroll
@@ -46,11 +49,11 @@ __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4&
         mb[j] = __float_as_uint(r1) & 0xffff0000u;
         lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
     }
-    hi = make_uint4((b[0] >> 16) | (b[1] & 0xffff0000u), (b[2] >> 16) | (b[3] & 0xffff0000u),
-                    (b[4] >> 16) | (b[5] & 0xffff0000u), (b[6] >> 16) | (b[7] & 0xffff0000u));
-    mid = make_uint4((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3], (mb[4] >> 16) | mb[5], (mb[6] >> 16) | mb[7]);
-    lo = make_uint4((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u),
-                    (lb[4] >> 16) | (lb[5] & 0xffff0000u), (lb[6] >> 16) | (lb[7] & 0xffff0000u));
+    // the upper halves of two dwords in one v_perm_b32 (the shift + and_or pair it replaces
+    // cost two vector instructions per packed dword)
+    hi = make_uint4(pk_hi16(b[0], b[1]), pk_hi16(b[2], b[3]), pk_hi16(b[4], b[5]), pk_hi16(b[6], b[7]));
+    mid = make_uint4(pk_hi16(mb[0], mb[1]), pk_hi16(mb[2], mb[3]), pk_hi16(mb[4], mb[5]), pk_hi16(mb[6], mb[7]));
+    lo = make_uint4(pk_hi16(lb[0], lb[1]), pk_hi16(lb[2], lb[3]), pk_hi16(lb[4], lb[5]), pk_hi16(lb[6], lb[7]));
 }
 
 // Epilogue stores as inline asm: hipcc then leaves them out of its vmcnt

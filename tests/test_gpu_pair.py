@@ -191,14 +191,15 @@ def test_pair_stagger_bitwise_equal(C, W, monkeypatch):
 @pytest.mark.parametrize("W", [224, 192, 136, 64, 8])
 def test_pair_role_split_kernel(W, monkeypatch):
     """The role-split kernel (PO2Q_PAIR_VARIANT + 20000, conv_pair_ab: conv-1 waves and conv-2
-    waves paired on each SIMD) is bit-identical to conv_pair on the plain chain (same splits, same
-    MFMA order per accumulator) and meets the bar with BN + activation epilogues (folded affine)."""
+    waves paired on each SIMD) equals conv_pair on the plain chain up to fp32 summation order
+    (conv_pair pairs the s2 tap of two planes in one k-step, conv_pair_ab keeps one k-step per
+    plane) and meets the bar with BN + activation epilogues (folded affine)."""
     x, w1, w2, e = make(2, 23, W, 29 + W, True, 16)
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", "23")
     ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", "20023")
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
-    assert torch.equal(y, ref)
+    assert nerr(y, ref) <= 1e-6, nerr(y, ref)
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", act1="relu", act2="silu", **e)
     ref = torch_chain(x, w1, w2, e, "relu", "silu", None, "po2+")
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)

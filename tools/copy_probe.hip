@@ -141,6 +141,50 @@ __global__ __launch_bounds__(256) void planes(const float* __restrict__ x, float
 }
 
 
+// planes with RPL image rows per step: a channel's RPL consecutive rows are one contiguous
+// run of RPL x W floats, so a step reads C runs of RPL x W x 4 bytes (and writes as many
+// LAG rows later) instead of C runs of one row.  C x RPL x W / 4 <= 64 x 14 x RPL float4.
+template <int RPL, int NTL, int NTS>
+__global__ __launch_bounds__(256) void planes_rpl(const float* __restrict__ x, float* __restrict__ y, int N, int C,
+                                                  int H, int W, int RB, int lag, int pad, int skew) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nseg = (H + RB - 1) / RB;
+    const int item = blockIdx.x * 4 + wave;
+    if (item >= N * nseg) return;
+    int seg = item % nseg;
+    const int n = item / nseg;
+    if (skew) seg = (seg + n) % nseg;  // concurrent blocks of different images at different rows
+    const long plane = (long)H * W + pad;  // pad: an artificial channel-plane stride
+    const float* xn = x + (long)n * C * plane;
+    float* yn = y + (long)n * C * plane;
+    const int RW4 = RPL * W / 4;  // float4 per channel run
+    const int per = C * RW4;
+    const int r0 = seg * RB, r1 = std::min(H, r0 + RB);
+    for (int r = r0; r < r1 + lag; r += RPL) {
+        f4 v[14 * RPL];
+#pragma unroll
+        for (int i = 0; i < 14 * RPL; ++i) {
+            const int e = i * 64 + lane;
+            const int c = e / RW4, q4 = e % RW4;
+            const long off = c * plane + (long)r * W + 4 * q4;
+            v[i] = (r < r1 && e < per && off < c * plane + (long)H * W) ? ld<NTL>(reinterpret_cast<const f4*>(xn + off))
+                                                                 : f4{0, 0, 0, 0};
+        }
+        const int ro = r - lag;
+        if (ro >= r0) {
+#pragma unroll
+            for (int i = 0; i < 14 * RPL; ++i) {
+                const int e = i * 64 + lane;
+                const int c = e / RW4, q4 = e % RW4;
+                const long off = c * plane + (long)ro * W + 4 * q4;
+                if (e < per && off < c * plane + (long)H * W) st<NTS>(reinterpret_cast<f4*>(yn + off), v[i]);
+            }
+        }
+    }
+}
+
+
 // ---- the conv's memory walk with no compute: LDS-DMA ring of PD rows, each landed
 // row read back (ds_read_b128) and stored to the same position of y.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, uint32_t bytes) {
@@ -275,10 +319,11 @@ int main(int argc, char** argv) {
     const double bytes = nf * 4.0;
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
     float *x, *y;
-    CK(hipMalloc(&x, nf * 4));
-    CK(hipMalloc(&y, nf * 4));
-    CK(hipMemset(x, 0, nf * 4));
-    CK(hipMemset(y, 0, nf * 4));
+    const long nalloc = nf + nf / 8;  // room for the padded plane strides of mode 4 (<= 1024 floats per plane)
+    CK(hipMalloc(&x, nalloc * 4));
+    CK(hipMalloc(&y, nalloc * 4));
+    CK(hipMemset(x, 0, nalloc * 4));
+    CK(hipMemset(y, 0, nalloc * 4));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -291,6 +336,33 @@ int main(int argc, char** argv) {
     char nm[128];
 
     const int mode = argc > 2 ? atoi(argv[2]) : 0;
+    if (mode == 4) {
+        // rows per step: stage 1 (16 ch @224) and stage 2 (32 ch @112, same bytes per row step)
+#define RPLP(R, L, S, CC, HH, RB, PAD, SK)                                                                              \
+    {                                                                                                          \
+        const int nseg = (HH + RB - 1) / RB;                                                                   \
+        const int NN = (int)(nf / ((long)CC * HH * HH));                                                       \
+        const int g = (NN * nseg + 3) / 4;                                                                     \
+        float ms = time_it(a, b, reps, [&] {                                                                   \
+            hipLaunchKernelGGL((planes_rpl<R, L, S>), dim3(g), dim3(256), 0, 0, x, y, NN, CC, HH, HH, RB, 2, PAD, SK); \
+        });                                                                                                    \
+        snprintf(nm, sizeof nm, "planes_C%d_H%d_RPL%d_ntl%d_nts%d_RB%d_pad%d_skew%d", CC, HH, R, L, S, RB, PAD, SK); \
+        report(nm, ms, 2.0);                                                                                   \
+    }
+        for (int rep2 = 0; rep2 < 2; ++rep2) {
+            {
+                float ms = time_it(a, b, reps, [&] { hipLaunchKernelGGL((gs<4, 1, 1>), dim3(4096), dim3(256), 0, 0, x4, y4, n4); });
+                report("gs_U4_ntl1_nts1_g4096", ms, 2.0);
+            }
+            RPLP(1, 1, 1, 16, 224, 28, 0, 0) RPLP(1, 1, 1, 16, 224, 28, 0, 1) RPLP(1, 1, 1, 16, 224, 28, 64, 0)
+            RPLP(1, 1, 1, 16, 224, 28, 256, 0) RPLP(1, 1, 1, 16, 224, 28, 1024, 0) RPLP(1, 1, 1, 16, 224, 28, 1024, 1)
+            RPLP(2, 1, 1, 16, 224, 28, 1024, 1) RPLP(1, 1, 1, 16, 224, 8, 0, 0) RPLP(1, 1, 1, 16, 224, 8, 64, 0)
+            RPLP(1, 1, 1, 32, 112, 28, 0, 0) RPLP(1, 1, 1, 32, 112, 28, 0, 1) RPLP(1, 1, 1, 32, 112, 28, 64, 0)
+            RPLP(1, 1, 1, 32, 112, 28, 1024, 0) RPLP(2, 1, 1, 32, 112, 28, 1024, 1)
+        }
+        CK(hipDeviceSynchronize());
+        return 0;
+    }
     if (mode == 3) {
 #define RING3(R, WR)                                                                                           \
     {                                                                                                          \
