@@ -404,28 +404,38 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         }
         // MFMAs: halo row j feeds output halo-index j+1 (r=0), j (r=1), j-1 (r=2)
         constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
+        // tap row rr of halo row j lands on segment output row j - rr: the edge steps (j < 2 or
+        // j >= rbe) skip the MFMAs whose output lies outside the segment.  One wave-uniform
+        // branch per step picks the guarded or the branch-free body: a test per tap row inside
+        // the k-step loop split the MFMA stream into blocks the scheduler could not interleave
+        // (26 branches and ~110 s_waitcnt per step in the loop's ISA).
+        auto mma = [&](auto G_) __attribute__((always_inline)) {
+            constexpr bool G = decltype(G_)::value;
 #pragma unroll
-        for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
-            bf16x8 af[3][NGW];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                for (int grp = 0; grp < NGW; ++grp)
-                    af[pl][grp] = __builtin_bit_cast(
-                        bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {
-                // tap row rr of halo row j lands on segment output row j - rr: skip the
-                // MFMAs of the edge rows whose output lies outside the segment (wave-uniform)
-                if (j - rr < 0 || j - rr >= rbe) continue;
+            for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
+                bf16x8 af[3][NGW];
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                     for (int grp = 0; grp < NGW; ++grp)
-                        acc[SL[rr]][grp] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr][ks], acc[SL[rr]][grp], 0, 0, 0);
+                        af[pl][grp] = __builtin_bit_cast(
+                            bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) {
+                    if (G && (j - rr < 0 || j - rr >= rbe)) continue;
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                        for (int grp = 0; grp < NGW; ++grp)
+                            acc[SL[rr]][grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr][ks],
+                                                                                      acc[SL[rr]][grp], 0, 0, 0);
+                }
             }
-        }
+        };
+        if (j >= 2 && j < rbe)
+            mma(std::false_type{});
+        else
+            mma(std::true_type{});
         // output halo-index j-1 (row p0 + j - 2) is complete
         constexpr int D = (S + 2) % 3;
         if constexpr (TT) {

@@ -5,6 +5,7 @@ so both libraries travel to the GPU box).  Each round runs every arm in its own 
 
   python tools/ab_pkg.py pair      # conv_pair stage 1 (bs = 256 @224): plain chain and BasicBlock form
   python tools/ab_pkg.py bench     # bench.py's chain (no CPU baseline / extra configs)
+  python tools/ab_pkg.py bench 3 PO2Q_PAIR_C32=1   # the working tree without / with an env setting
 """
 import json
 import os
@@ -42,9 +43,10 @@ print("AB " + json.dumps(out))
 '''
 
 
-def run_arm(root, what):
+def run_arm(root, what, extra=None):
     env = dict(os.environ)
     env.pop("PO2Q_LIB", None)
+    env.update(extra or {})
     if what == "pair":
         cmd = [sys.executable, "-c", PAIR]
     else:
@@ -65,11 +67,15 @@ def run_arm(root, what):
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "pair"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    arms = {"new": ROOT, "old": os.path.join(ROOT, "ab_old")}
+    if len(sys.argv) > 3:  # env A/B on the working tree
+        k, v = sys.argv[3].split("=", 1)
+        arms = {"base": (ROOT, {}), sys.argv[3]: (ROOT, {k: v})}
+    else:
+        arms = {"new": (ROOT, {}), "old": (os.path.join(ROOT, "ab_old"), {})}
     res = {k: [] for k in arms}
     for r in range(rounds):
-        for k, root in (arms.items() if r % 2 == 0 else reversed(list(arms.items()))):
-            v = run_arm(root, what)
+        for k, (root, extra) in (arms.items() if r % 2 == 0 else reversed(list(arms.items()))):
+            v = run_arm(root, what, extra)
             res[k].append(v)
             print(json.dumps({"round": r, "arm": k, **v}), flush=True)
     for k, vs in res.items():
