@@ -124,14 +124,17 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nw = (int)(blockDim.x >> 6);
     const int rawslot = CC * a.Wp * 4;
-    const int yslot = 3 * a.YPL;
+    // the intermediate planes are sized for the widest image (7 waves): a compile-time pitch turns
+    // every slot / plane offset of the fragment reads and epilogue writes into an immediate
+    constexpr int YPL = (7 * SW + 3) * 2 * CC;
+    constexpr int yslot = 3 * YPL;
     unsigned char* raw = lds;                                   // PD x [C][Wp] fp32 (x rows)
     unsigned char* yr = raw + PD * rawslot;                     // 2 x 3 planes (intermediate, split)
     unsigned char* slab = yr + 2 * yslot + wave * (3 * PL);     // this wave's x planes
     unsigned char* resr = yr + 2 * yslot + nw * (3 * PL) + wave * (PD * kQResSlot);
     uint4* wl2 = reinterpret_cast<uint4*>(yr + 2 * yslot + nw * (3 * PL) + (RES ? nw * PD * kQResSlot : 0));
     const int zero_off = WC * CC * 2;
-    const int yzero = (a.Wp + 2) * (2 * CC);                    // zero slot of a shared plane
+    constexpr int yzero = (7 * SW + 2) * (2 * CC);              // zero slot of a shared plane
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
@@ -222,9 +225,9 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                         yoff[grp][ks] = yoct<CC>(yp, o);
                     } else {
                         aoff[grp][ks] = xa<CC>(xp, o) + (g >= 2 ? PL : 0);
-                        yoff[grp][ks] = yoct<CC>(yp, o) + (g >= 2 ? a.YPL : 0);
+                        yoff[grp][ks] = yoct<CC>(yp, o) + (g >= 2 ? YPL : 0);
                         aoff2[grp] = g >= 2 ? zero_off : xa<CC>(xp, o) + 2 * PL;
-                        yoff2[grp] = g >= 2 ? yzero : yoct<CC>(yp, o) + 2 * a.YPL;
+                        yoff2[grp] = g >= 2 ? yzero : yoct<CC>(yp, o) + 2 * YPL;
                     }
                 } else {  // ks = tap s, k = the 32 channels (octet g)
                     aoff[grp][ks] = xa<CC>(16 * grp + p + ks, g);
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     if (CC == 16 && ks == 1)
                         off = pl == 0 ? (TR ? aoff[grp][1] : yoff[grp][1]) : (TR ? aoff2[grp] : yoff2[grp]);
                     else
-                        off = TR ? pl * PL + aoff[grp][ks] : pl * a.YPL + yoff[grp][ks];
+                        off = TR ? pl * PL + aoff[grp][ks] : pl * YPL + yoff[grp][ks];
                     af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + off));
                 }
 #pragma unroll
@@ -297,9 +300,12 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                         for (int grp = 0; grp < NG; ++grp) {
                             if (pl >= np) continue;
-                            acc[SL[rr]][grp][nt] =
-                                TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], acc[SL[rr]][grp][nt], 0, 0, 0)
-                                   : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, acc[SL[rr]][grp][nt], 0, 0, 0);
+                            // slot SL[0] (output row j + 1) starts at this step: its first MFMA takes a
+                            // zero accumulator, so the epilogues need not clear the slot they retire
+                            const floatx4 c = (rr == 0 && ks == 0 && pl == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
+                                                                             : acc[SL[rr]][grp][nt];
+                            acc[SL[rr]][grp][nt] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], c, 0, 0, 0)
+                                                      : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, c, 0, 0, 0);
                         }
                 }
         }
@@ -345,7 +351,6 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     const int q = q0 + ql;
                     rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
-                acc2[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
         if (CC == 16 && !a.halves) {
@@ -477,11 +482,10 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     const int wo = yoct<CC>(q + 1, (4 * nt + g) >> 1) + 8 * (g & 1);
                     *reinterpret_cast<uint2*>(yw + wo) =
                         make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-                    *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
+                    *reinterpret_cast<uint2*>(yw + YPL + wo) =
                         make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
-                    *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
+                    *reinterpret_cast<uint2*>(yw + 2 * YPL + wo) =
                         make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
-                    acc1[D][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
                 }
             }
         }
@@ -926,7 +930,7 @@ static size_t pair_lds(int C, int waves, int pd, bool res) {
     const int sw = 512 / C, wp = sw * waves;
     const int plane = (sw + 2) * 2 * C + 32;
     const int nf = 3 * (C == 16 ? 2 : 3) * (C / 16);
-    return (size_t)pd * C * wp * 4 + 2 * 3 * (size_t)(wp + 3) * 2 * C + (size_t)waves * 3 * plane +
+    return (size_t)pd * C * wp * 4 + 2 * 3 * (size_t)(7 * sw + 3) * 2 * C + (size_t)waves * 3 * plane +
            (res ? (size_t)waves * pd * kQResSlot : 0) + (C == 32 ? (size_t)nf * 64 * 16 : 0);
 }
 
@@ -1112,7 +1116,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     po2q::PairArgs a;
     a.N = (int)N; a.H = (int)H; a.W = (int)W;
     a.Wp = (512 / (int)C) * pp.waves;
-    a.YPL = (a.Wp + 3) * 2 * (int)C;
+    a.YPL = (7 * (512 / (int)C) + 3) * 2 * (int)C;  // the kernel's compile-time plane pitch
     a.RB = pp.RB; a.nseg = pp.nseg; a.items = (int)(N * pp.nseg);
     a.remap = (pp.blocks % 8 == 0) ? 1 : 0;
     const int lo = fsr - (1 << (bits - 1)), hi = fsr - 1;
