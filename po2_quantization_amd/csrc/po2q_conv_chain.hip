@@ -219,6 +219,89 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     };
     load_bw(a.layer[0]);
 
+    // C = 16: the 27 sixteen-channel units of an output pixel (3 tap rows x 3 taps x 3 planes) in 14
+    // k-steps instead of 18: per tap row (s0 | s1) of each plane (9 steps), then the nine s2 units
+    // paired across planes AND tap rows -- every tap row feeds the same accumulator here --:
+    // (r0 hi | r0 mid), (r0 lo | r1 hi), (r1 mid | r1 lo), (r2 hi | r2 mid), (r2 lo | zero).  The
+    // pairs' B fragments hold the s2 weights of the two tap rows in their two k-halves; they are
+    // built per layer from the pack's (s2 | zero) fragments with v_permlane32_swap (lanes 32-63 of
+    // a fragment take lanes 0-31 of the other).  One plane read per MFMA, issued PD16 steps ahead;
+    // FULL (the CIFAR stages) orders the MFMAs k-step major, so consecutive MFMAs accumulate into
+    // different groups (the group-major order of the other shapes keeps them under 256 VGPRs).
+    auto mma16 = [&](floatx4 (&acc)[MG]) __attribute__((always_inline)) {
+        constexpr int T1 = 14, S1 = MG * T1, PD16 = 10;
+        bf16x8 bq[8];
+        auto pair = [&](const bf16x8& lo, const bf16x8& hi) __attribute__((always_inline)) {
+            const uint4 u = __builtin_bit_cast(uint4, lo), v = __builtin_bit_cast(uint4, hi);
+            uint4 r;
+            r.x = __builtin_amdgcn_permlane32_swap(u.x, v.x, false, false)[0];
+            r.y = __builtin_amdgcn_permlane32_swap(u.y, v.y, false, false)[0];
+            r.z = __builtin_amdgcn_permlane32_swap(u.z, v.z, false, false)[0];
+            r.w = __builtin_amdgcn_permlane32_swap(u.w, v.w, false, false)[0];
+            return __builtin_bit_cast(bf16x8, r);
+        };
+        bq[0] = bw[0];
+        bq[1] = bw[2];
+        bq[2] = bw[4];
+        bq[3] = pair(bw[1], bw[1]);  // (r0 hi | r0 mid)
+        bq[4] = pair(bw[1], bw[3]);  // (r0 lo | r1 hi)
+        bq[5] = pair(bw[3], bw[3]);  // (r1 mid | r1 lo)
+        bq[6] = pair(bw[5], bw[5]);  // (r2 hi | r2 mid)
+        bq[7] = bw[5];               // (r2 lo | zero)
+        // Addresses: the unswizzled C = 16 plane is linear in the pixel (32 bytes each), so a read is
+        // one VGPR add: a per-group lane base plus a uniform offset (tap row, plane; SGPR) for the
+        // (s0 | s1) steps, or plus a per-lane offset (the two k-halves' tap rows / planes) for the
+        // paired s2 steps.  The last pair's zero half reads the r2 lo unit again (finite: the split
+        // clamps mid / lo) against zero weights, so it needs no zero slot.
+        int lb[MG], dsel[5];
+#pragma unroll
+        for (int gi = 0; gi < MG; ++gi) lb[gi] = (pp0[gi] + 2) * 32 + 16 * (g4 & 1);  // tap s = 2
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int ua = 2 * u, ub = u == 4 ? 8 : 2 * u + 1;
+            const int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
+            dsel[u] = g4 < 2 ? ra * PW * 32 + pa * a.PL : rb * PW * 32 + pb * a.PL;
+        }
+        const int s01 = ((g4 >> 1) - 2) * 32;  // tap (g4 >> 1) relative to the s = 2 base
+        auto addr = [&](auto ST_) __attribute__((always_inline)) {
+            constexpr int st = decltype(ST_)::value;
+            constexpr int t = FULL ? st / MG : st % T1, gi = FULL ? st % MG : st / T1;  // FULL: k-step major
+            if constexpr (S16) {  // A/B layout: the generic address
+                if constexpr (t < 9) {
+                    constexpr int r = t / 3, pl = t % 3;
+                    const int s = g4 >> 1;
+                    return pl * a.PL + ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1);
+                } else {
+                    constexpr int ua = 2 * (t - 9), ub = t == 13 ? 8 : ua + 1;
+                    constexpr int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
+                    if (g4 < 2) return pa * a.PL + ch_addr<C, W8, S16>(pp0[gi] + ra * PW + 2, px0[gi] + 2, g4 & 1);
+                    return pb * a.PL + ch_addr<C, W8, S16>(pp0[gi] + rb * PW + 2, px0[gi] + 2, g4 & 1);
+                }
+            } else if constexpr (t < 9) {
+                constexpr int r = t / 3, pl = t % 3;
+                return lb[gi] + s01 + (r * PW * 32 + pl * a.PL);
+            } else {
+                return lb[gi] + dsel[t - 9];
+            }
+        };
+        bf16x8 ring[PD16 + 1];
+        auto issue = [&](auto ST_) __attribute__((always_inline)) {
+            constexpr int st = decltype(ST_)::value;
+            if constexpr (st < S1)
+                ring[st % (PD16 + 1)] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + addr(ST_)));
+        };
+        auto step = [&](auto ST_) __attribute__((always_inline)) {
+            constexpr int st = decltype(ST_)::value;
+            issue(std::integral_constant<int, st + PD16>{});
+            constexpr int t = FULL ? st / MG : st % T1, gi = FULL ? st % MG : st / T1;  // FULL: k-step major
+            constexpr int bi = t < 9 ? t / 3 : 3 + (t - 9);
+            acc[gi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[bi], ring[st % (PD16 + 1)], acc[gi], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for<PD16>(issue);
+        static_for<S1>(step);
+    };
+
     for (int l = 0; l < a.L; ++l) {
         const ChainLayer& ly = a.layer[l];
         // this layer's epilogue constants: loaded now, consumed after the MFMA phase
@@ -239,6 +322,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         floatx4 acc[MG];
 #pragma unroll
         for (int gi = 0; gi < MG; ++gi) acc[gi] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (C == 16) {
+            mma16(acc);
+        } else {
         bf16x8 ring[PD + 1][3];
         auto issue = [&](auto ST_) __attribute__((always_inline)) {
             constexpr int st = decltype(ST_)::value;
@@ -262,6 +348,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         };
         static_for<PD>(issue);
         static_for<S>(step);
+        }
 
         // the next layer's B fragments go out now (the last layer reloads its own: no branch, so
         // the epilogue's wait for this layer's constants stays a counted vmcnt, not vmcnt(0))

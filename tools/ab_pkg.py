@@ -5,6 +5,7 @@ so both libraries travel to the GPU box).  Each round runs every arm in its own 
 
   python tools/ab_pkg.py pair      # conv_pair stage 1 (bs = 256 @224): plain chain and BasicBlock form
   python tools/ab_pkg.py bench     # bench.py's chain (no CPU baseline / extra configs)
+  python tools/ab_pkg.py cifar     # bench.py's config-2 line (ResNet56 @32 chain kernels, HIP graph)
   python tools/ab_pkg.py bench 3 PO2Q_PAIR_C32=1   # the working tree without / with an env setting
 """
 import json
@@ -49,6 +50,8 @@ def run_arm(root, what, extra=None):
     env.update(extra or {})
     if what == "pair":
         cmd = [sys.executable, "-c", PAIR]
+    elif what == "cifar":  # the config-2 chain (ResNet56 @32, HIP graph) of bench.py's extra line
+        cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-models"]
     else:
         cmd = [sys.executable, "bench.py", "--steps", "30", "--warmup", "3", "--no-cpu-baseline", "--no-cifar",
                "--no-models"]
@@ -60,6 +63,10 @@ def run_arm(root, what, extra=None):
             return json.loads(line[3:])
         if line.startswith("{") and '"metric"' in line:
             d = json.loads(line)
+            if what == "cifar":
+                c = d["config2_cifar32"]
+                return {"img_s": c["value"], "ms_per_step": c["ms_per_step"],
+                        "chain16_ms": c["roofline"]["avg_launch_ms"]}
             return {"img_s": d["value"], "ms_per_step": d["ms_per_step"]}
     raise RuntimeError("no result from " + root)
 
