@@ -59,7 +59,7 @@ struct PairArgs {
     int act1, act2;
     const float* res;  // RES: residual [N, C, H, W] added before act2
     int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
-    int halves;        // C = 16, 1: store 64-byte half lines as the MFMA layout holds them (A/B knob)
+    int halves;        // unused (the half-line A/B knob of round 2: C = 16 always stores whole lines)
     int stg;           // 1: the stagger (STG) kernel for the forms without a residual
 };
 
@@ -195,9 +195,12 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     // (side, channel) from the neighbours' columns of the shared raw row (zero outside)
     const int sc = lane % SW, so = lane / SW;
     const int wa_i = xa<CC>(sc + 1, so);
-    const int hside = (lane / CC) & 1, hch = lane % CC;
+    // (lanes 2C.. -- C = 16 -- repeat lanes 0 .. 2C-1: they read and write the same halo values,
+    // so the halo split needs no divergent branch)
+    const int hl = lane % (2 * CC);
+    const int hside = (hl / CC) & 1, hch = hl % CC;
     const int hq = hside ? q0 + SW : q0 - 1;
-    const bool h_ok = lane < 2 * CC && hq >= 0 && hq < a.W;
+    const bool h_ok = hq >= 0 && hq < a.W;
     const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
     const int rdx0 = (so * 8) * (a.Wp * 4) + (q0 + sc) * 4;
     const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
@@ -347,13 +350,13 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                     for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
                 }
                 vv[nt][grp] = v;
-                if (CC != 16 || a.halves) {
+                if constexpr (CC != 16) {
                     const int q = q0 + ql;
                     rows_store<(NTS & 1) != 0>(ry, (orow && q < a.W) ? (yrow + (uint32_t)q) * 4u : 0x7fffffffu, v);
                 }
             }
         }
-        if (CC == 16 && !a.halves) {
+        if constexpr (CC == 16) {
             // Whole 128-byte lines per store: lane L holds pixels 4g .. 4g + 3 (vv[0][0]) and
             // 16 + 4g .. (vv[0][1]) of channel L & 15.  One row_ror:8 DPP exchange within each
             // 16-lane row gives store A channels 0-7 (lanes with bit 3 set take channel L & 7's
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         *reinterpret_cast<uint4*>(slab + wa_i) = hi;
         *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
         *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
-        if (lane < 2 * CC) {
+        {
             uint16_t h16, m16, l16;
             split1(h_ok ? hx : 0u, h16, m16, l16);
             *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
@@ -432,7 +435,9 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         }
 
         // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
-        if ((DBG & 1) == 0 && j >= 3)
+        // (unconditional: in steps 0-2 it reads the zeroed ring slots and its outputs are dropped --
+        // no branch, so its MFMAs interleave with the epilogue-2 and x-split vector work below)
+        if constexpr ((DBG & 1) == 0)
             mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
         if (!late) {
             epi2(S_, j);
@@ -1029,7 +1034,7 @@ void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C
         stg = v >= 20000 ? 2 : (v >= 10000 ? 1 : 0);  // + 10000: the stagger kernel (STG) where no residual is
                                                       // added; + 20000: the role-split kernel (conv_pair_ab)
         v %= 10000;
-        halves = v >= 1000 ? 1 : 0;  // + 1000: 64-byte half-line stores (C = 16)
+        halves = v >= 1000 ? 1 : 0;  // + 1000: accepted, no effect (half-line stores were dropped in round 3)
         v %= 1000;
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
