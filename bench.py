@@ -557,7 +557,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pair", action="store_true",
-                    help="run every conv as its own launch (no stage-1 conv1->conv2 pair kernel)")
+                    help="run every conv as its own launch (no conv1->conv2 pair kernel in stages 1-2)")
     ap.add_argument("--no-s2ds", action="store_true",
                     help="run a stage's stride-2 conv1 and its 1x1 shortcut as two launches (each reads x)")
     ap.add_argument("--no-pack-batch", action="store_true",
@@ -636,6 +636,8 @@ def main():
     # dominant op (HIP events on its stream): the stage-1 conv pair (conv1 -> conv2 of a block
     # in one launch) when the chain runs pairs, else the fused quantize+conv of the timed shape
     pair_used = chain.pairable(0, x)
+    pair32_used = chain.pair and args.quantizer in ("po2", "po2+") and \
+        _lib.pair_supported((B, 32, Hs // 2, Hs // 2), args.bits, args.quantizer)
     s2ds_used = chain.s2ds and args.quantizer in ("po2", "po2+") and \
         _lib.s2ds_supported((B, 16, Hs, Hs), args.bits, args.quantizer)
     xl = torch.relu(torch.randn(args.batch, 16, args.image, args.image, device=dev))
@@ -732,13 +734,15 @@ def main():
         "dtype": "fp32" if prec == "fp32" else "fp32(bf16x3)", "data": "synthetic",
         "config": {"workload": "%s quantized-conv chain: %d fused %s-%dbit quantize+conv fwd + head%s%s%s%s"
                                % (args.model, len(chain.layers), args.quantizer, args.bits,
-                                  " (stage-1 conv1->conv2 pairs as one launch each)" if pair_used else "",
+                                  (" (stage-1%s conv1->conv2 pairs as one launch each)"
+                                   % (" and stage-2" if pair32_used else "")) if pair_used else "",
                                   " (stride-2 conv1 + 1x1 shortcut of stages 2-3 as one launch each)"
                                   if s2ds_used else "",
                                   " (weight packs of the single-conv layers batched: one launch per 24)"
                                   if chain.packed is not None else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "conv_pairs": pair_used,
+                   "conv_pairs_stage2": pair32_used,
                    "s2ds": s2ds_used,
                    "pack_batch": chain.packed is not None,
                    "autotune": _lib.benchmark,

@@ -242,7 +242,8 @@ int po2q_dilate_f32(const float* src, float* dst, int64_t N, int64_t C, int64_t 
  * po2q_qconv2d_pair_f32 takes C in {16, 32}, W % 4 == 0, W <= 7 * 512 / C (224 for C = 16,
  * 112 for C = 32), mode po2 / po2+ with the exponent window inside bf16's range.
  * po2q_qconv2d_pair_supported: 1 when it takes the shape AND is the faster path (C = 16 with
- * W >= 128; C = 32 only when PO2Q_PAIR_C32 is set; otherwise two single-conv calls).
+ * W > 96, C = 32 with W > 48 -- PO2Q_PAIR_C32=0 turns C = 32 off; otherwise two single-conv
+ * calls).
  */
 int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int bits, int fsr, int mode);
 int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, float* y,

@@ -1085,10 +1085,15 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
     // below 4 waves per block a block is too narrow to hide its per-row latency: two
     // single-conv launches are faster there (ResNet56 @32: 2.6 vs 2.0 ms per forward)
     if ((C == 16 || C == 32) && W <= 3 * (512 / C)) return 0;
-    // C = 32 (stage 2 @112): 0.366 ms per pair alone but 0.418 ms inside the ResNet56 chain,
-    // against 2 x 0.197 ms for the single-conv kernel there (profiles/r02_v7_kernel_stats.csv):
-    // the pair is not the faster path, so the advisory says no (the kernel stays callable)
-    if (C == 32 && !getenv("PO2Q_PAIR_C32")) return 0;  // PO2Q_PAIR_C32=1: advise it anyway (A/B runs)
+    // C = 32 (stage 2 @112): round 2 measured the pair slower inside the ResNet56 chain (0.418 ms
+    // against 2 x 0.197 for the single-conv kernel, profiles/r02_v7_kernel_stats.csv); after the
+    // round-3 instruction diet it is 0.339 ms alone and the chain with stage-2 pairs runs 24.0k
+    // against 23.4k img/s, 4 of 4 interleaved rounds on one box (profiles/r03_ab_stage2_pairs_v2.jsonl),
+    // so it is advised.  PO2Q_PAIR_C32=0 turns the advice off (A/B runs).
+    if (C == 32) {
+        const char* e = getenv("PO2Q_PAIR_C32");
+        if (e && e[0] == '0') return 0;
+    }
     po2q::PairPlan pp;
     int pd, nts, prio, halves, stg;
     pair_variant(pd, nts, prio, halves, stg, C);

@@ -108,7 +108,8 @@ def test_pair_rejects():
     w = torch.randn(64, 64, 3, 3, device=DEV)
     assert not _lib.pair_supported(x.shape)
     assert _lib.pair_supported((256, 16, 224, 224)) and not _lib.pair_supported((256, 16, 32, 32))
-    assert not _lib.pair_supported((256, 32, 112, 112))  # callable, but not the faster path in the chain
+    assert _lib.pair_supported((256, 32, 112, 112))  # stage 2 @112: advised since round 3
+    assert not _lib.pair_supported((256, 32, 16, 16))  # CIFAR stage 2: two single-conv launches (or the chain)
     with pytest.raises(_lib.Po2qError, match="16 or 32 channels"):
         _lib.qconv2d_pair(x, w, w)
     x = torch.randn(1, 16, 8, 10, device=DEV)
