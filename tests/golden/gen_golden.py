@@ -264,13 +264,39 @@ def gen_models_wide():
     print("models_wide.npz:", sorted(out))
 
 
+VIT256 = ("mobilevit", 256, 2, "po2+", 2, 5, 1000)  # config 5: MobileViT-XS @256 (ImageNet head), po2+ 2-bit
+
+
+def gen_vit256():
+    """models_vit256.npz: QAT-mode eval logits of MobileViT-XS @256x256 (BASELINE config 5, weights
+    quantized: the reference quantizes no activations) -- reference models/mobile_vit.py:131-311 at
+    the size the bench runs.  The input is NOT stored: the test regenerates it from the seed
+    (torch CPU generator), so the fixture stays small."""
+    from models.model import get_model
+    from utils.quantizers import quantizer_dict
+
+    mt, sz, bs, q, bits, seed, nc = VIT256
+    m = get_model(mt, nc, quantizer_dict[q], bits, (sz, sz))
+    seeded_fill_(m, seed=7)
+    m.eval()
+    x = torch.randn(bs, 3, sz, sz, generator=torch.Generator().manual_seed(seed))
+    with torch.no_grad():
+        logits = m(x)
+    tag = "%s@%d/%s/%d" % (mt, sz, q, bits)
+    out = {"logits/" + tag: logits.numpy(), "x_sum/" + tag: np.array(float(x.double().sum()))}
+    np.savez_compressed(os.path.join(HERE, "models_vit256.npz"), **out)
+    print("models_vit256.npz:", sorted(out), logits.shape)
+
+
 def main():
     sys.path.insert(0, REF)
     thr = json.load(open(os.path.join(HERE, "po2_thresholds.json")))["modes"]
     torch.set_num_threads(8)
-    parts = sys.argv[1:] or ["quant", "conv", "lin", "models", "wide"]  # e.g. `gen_golden.py lin`
+    parts = sys.argv[1:] or ["quant", "conv", "lin", "models", "wide", "vit256"]  # e.g. `gen_golden.py lin`
     if "wide" in parts:
         gen_models_wide()
+    if "vit256" in parts:
+        gen_vit256()
     if "quant" in parts:
         gen_quant(thr)
     if "conv" in parts:

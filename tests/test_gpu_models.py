@@ -126,12 +126,12 @@ def test_layer_quantization_error_vs_oracle():
 def test_wide_resnet_logits_through_fused_block_kernels(tag, pair_c32, monkeypatch):
     """Reference logits (tests/golden/models_wide.npz, generated by running the reference's
     ResNet, models/resnet.py:55-71,150-163,190-201) through the drop-in's eval forward at a width
-    where BasicBlock.forward takes the fused-block kernels: the stage-1 conv pair (and, with
-    PO2Q_PAIR_C32, the stage-2 pairs) and the stride-2 + shortcut kernel.  Asserts they ran."""
+    where BasicBlock.forward takes the fused-block kernels: the stage-1 conv pair, the stage-2 pairs
+    (advised by default; PO2Q_PAIR_C32=0 turns them off) and the stride-2 + shortcut kernel.  Asserts
+    they ran."""
     from po2_quantization_amd import _lib
 
-    if pair_c32:
-        monkeypatch.setenv("PO2Q_PAIR_C32", "1")
+    monkeypatch.setenv("PO2Q_PAIR_C32", "1" if pair_c32 else "0")  # stage-2 pairs advised by default
     d = load_npz("models_wide.npz")
     spec, q, bits = tag.split("/")
     mt, sz = spec.split("@")
@@ -155,6 +155,22 @@ def test_wide_resnet_logits_through_fused_block_kernels(tag, pair_c32, monkeypat
     with torch.no_grad():
         y = m(torch.from_numpy(d["x/" + tag]).to(DEV)).cpu().numpy()
     assert calls["pair16"] == nb and calls["s2ds"] >= 1, calls
-    if pair_c32:
-        assert calls["pair32"] == nb - 1, calls
+    assert calls["pair32"] == (nb - 1 if pair_c32 else 0), calls
+    assert normwise_err(y, d["logits/" + tag]) <= LOGIT_TOL, normwise_err(y, d["logits/" + tag])
+
+
+def test_mobilevit_256_logits_config5():
+    """BASELINE config 5 at its own size: MobileViT-XS @256x256, 1000 classes, po2+ 2-bit QAT-mode
+    weights (the reference quantizes no activations), eval forward with every conv + BN + act native,
+    against the reference's logits (tests/golden/models_vit256.npz; reference models/mobile_vit.py:
+    131-311).  The input comes from its seed (torch CPU generator), checked by its sum."""
+    d = load_npz("models_vit256.npz")
+    tag = "mobilevit@256/po2+/2"
+    x = torch.randn(2, 3, 256, 256, generator=torch.Generator().manual_seed(5))
+    assert abs(float(x.double().sum()) - float(d["x_sum/" + tag])) <= 1e-6 * abs(float(d["x_sum/" + tag])) + 1e-3
+    m = get_model("mobilevit", 1000, quantizer_dict["po2+"], 2, (256, 256))
+    seeded_fill_(m, seed=7)
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu().numpy()
     assert normwise_err(y, d["logits/" + tag]) <= LOGIT_TOL, normwise_err(y, d["logits/" + tag])

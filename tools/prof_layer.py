@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--tile", default=None)
     ap.add_argument("--precision", default="auto")
     ap.add_argument("--plan", type=int, default=None, help="candidate plan index (po2q_qconv2d_plans)")
-    ap.add_argument("--pair", action="store_true", help="the stage-1 conv pair kernel (conv_pair16) instead")
+    ap.add_argument("--pair", action="store_true", help="the conv pair kernel (conv_pair<C>: stage 1 or 2) instead")
     args = ap.parse_args()
     if args.tile:
         os.environ["PO2Q_X3_TILE"] = args.tile
@@ -32,11 +32,11 @@ def main():
 
     C, H, K, R, st, pad = (int(v) for v in args.shape.split(","))
     dev = torch.device("cuda:0")
-    if args.pair:  # PLAN key = the bench's roofline traffic key for the pair
-        x = torch.randn(args.batch, 16, H, H, device=dev)
-        w1 = torch.randn(16, 16, 3, 3, device=dev) * 0.1
-        w2 = torch.randn(16, 16, 3, 3, device=dev) * 0.1
-        print("PLAN pair16 %dx%d bs=%d" % (H, H, args.batch), flush=True)
+    if args.pair:  # PLAN key = the bench's roofline traffic key for the pair (C = 16 or 32 from --shape)
+        x = torch.randn(args.batch, C, H, H, device=dev)
+        w1 = torch.randn(C, C, 3, 3, device=dev) * 0.1
+        w2 = torch.randn(C, C, 3, 3, device=dev) * 0.1
+        print("PLAN pair%d %dx%d bs=%d" % (C, H, H, args.batch), flush=True)
         for _ in range(args.iters):
             _lib.qconv2d_pair(x, w1, w2, 4, "po2")
         torch.cuda.synchronize()
