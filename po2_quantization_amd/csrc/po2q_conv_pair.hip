@@ -286,10 +286,13 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                         off = TR ? pl * PL + aoff[grp][ks] : pl * YPL + yoff[grp][ks];
                     af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + off));
                 }
+            // tap row 2 first: it feeds the slot that completes this step, so its epilogue can
+            // start while the other tap rows' MFMAs of the last k-step still run
 #pragma unroll
-            for (int rr = 0; rr < 3; ++rr)
+            for (int r3 = 0; r3 < 3; ++r3)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
+                    const int rr = 2 - r3;
                     const int f = (rr * KS + ks) * NT + nt;
                     bf16x8 b;
                     if constexpr (TR)
