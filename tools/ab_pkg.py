@@ -1,6 +1,6 @@
 """Same-box A/B of two builds of the package (tuning aid, GPU only): the working tree and a
-second build kept under ab_old/ (a git worktree of an earlier commit, built there and copied in,
-so both libraries travel to the GPU box).  Each round runs every arm in its own process
+second build kept under ab_old/ (a git worktree of an earlier commit, built there and copied in by
+tools/make_ab_old.sh, so both libraries travel to the GPU box; delete it when done).  Each round runs every arm in its own process
 (both packages are named po2_quantization_amd), alternating arms, so box drift hits both alike.
 
   python tools/ab_pkg.py pair      # conv_pair stage 1 (bs = 256 @224): plain chain and BasicBlock form
