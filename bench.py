@@ -542,7 +542,7 @@ def model_cpu_baseline(m, image, seconds, label):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)  # ~0.6 s timed at 224: long enough for an external sampler
+    ap.add_argument("--steps", type=int, default=100)  # ~1.1 s timed at 224: long enough for an external sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--global-batch", type=int, default=None,
