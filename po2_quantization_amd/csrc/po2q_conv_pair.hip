@@ -1122,6 +1122,15 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     po2q::PairPlan pp;
     int pd, nts, prio, halves, stg;
     pair_variant(pd, nts, prio, halves, stg, C);
+    if (residual && C == 16 && !getenv("PO2Q_PAIR_VARIANT")) {
+        // the BasicBlock form re-reads x as the residual five steps after its row DMA: with
+        // temporal x loads that read hits L2, with non-temporal ones it goes back to memory.
+        // Variant 21 (temporal x loads, non-temporal stores, no priority): 0.514 vs 0.551 ms,
+        // 3 of 3 interleaved rounds (profiles/r03_ab_pair_res_temporal_x.jsonl)
+        pd = 2;
+        nts = 1;
+        prio = 0;
+    }
     if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, residual != nullptr, pd, nts)) {
         po2q::set_error("po2q: pair: no plan for this shape");
         return PO2Q_ERR_UNSUPPORTED;
