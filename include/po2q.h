@@ -236,8 +236,9 @@ int po2q_dilate_f32(const float* src, float* dst, int64_t N, int64_t C, int64_t 
  * models/resnet.py:55-71; each conv is QuantizedConv2d.forward, models/quantized_conv.py:
  * 32-38; stage 2 takes it too): 3x3 / stride 1 / pad 1, C -> C -> C channels with C = 16 or
  * 32, x [N,C,H,W], w1 / w2 [C,C,3,3] quantized with the same (bits, fsr, mode):
- *   y = act2(conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 (+ residual))
  *   h = act1((conv(x, Q(w1)) + bias1) * post_scale1 + post_shift1)
+ *   y = act2((conv(h, Q(w2)) + bias2) * post_scale2 + post_shift2 + residual)
+ * (the affine first, then the residual add, then the activation; a NULL residual adds nothing)
  * (every pointer but x, w1, w2, y may be NULL).  h never leaves the chip.  No workspace.
  * po2q_qconv2d_pair_f32 takes C in {16, 32}, W % 4 == 0, W <= 7 * 512 / C (224 for C = 16,
  * 112 for C = 32), mode po2 / po2+ with the exponent window inside bf16's range.
@@ -336,10 +337,15 @@ void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan);
  * workspace[i] (>= po2q_qconv2d_plan_workspace_bytes) -- the bf16x3 packs in
  * ceil(n / 24) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
  * from that workspace (w is read only by plans that stage their weight in-kernel); on one
- * stream the pair equals po2q_qconv2d_plan_run bit for bit.
+ * stream the pair equals po2q_qconv2d_plan_run bit for bit.  The plans may differ in bits /
+ * fsr / mode; depthwise plans join the batched launches too (their plain quantized copy).
+ * po2q_qconv2d_plan_packs_weight: 1 when plan's conv reads a packed workspace (a pack
+ * launch is due before po2q_qconv2d_plan_run_packed), 0 when the kernel stages the weight
+ * itself or reads it as given (nothing to batch), < 0 on error.
  */
 int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, const float* const* w,
                                  void* const* workspace, const size_t* workspace_bytes, void* stream);
+int po2q_qconv2d_plan_packs_weight(const po2q_conv_plan* plan);
 int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias,
                                  float* y, const float* post_scale, const float* post_shift,
                                  const float* residual, int act, const void* workspace,

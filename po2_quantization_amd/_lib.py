@@ -57,6 +57,7 @@ EXPORTS = (
     "po2q_qconv2d_s2ds_f32",
     "po2q_qconv2d_plan_pack_batch",
     "po2q_qconv2d_plan_run_packed",
+    "po2q_qconv2d_plan_packs_weight",
     "po2q_dilate_f32",
     "po2q_qconv2d_chain_supported",
     "po2q_qconv2d_chain_workspace_bytes",
@@ -162,6 +163,8 @@ def load():
                                                ctypes.POINTER(sz), p]
     L.po2q_qconv2d_plan_run_packed.restype = i32
     L.po2q_qconv2d_plan_run_packed.argtypes = [p] * 8 + [i32, p, sz, p]
+    L.po2q_qconv2d_plan_packs_weight.restype = i32
+    L.po2q_qconv2d_plan_packs_weight.argtypes = [p]
     L.po2q_qconv2d_chain_supported.restype = i32
     L.po2q_qconv2d_chain_supported.argtypes = [i64] * 4 + [i32] * 4
     L.po2q_qconv2d_chain_workspace_bytes.restype = sz
@@ -198,9 +201,13 @@ def _workspace(nbytes, dev):
 def restated_quantize(w, bits, mode, fsr=1):
     """PO2 / PO2+ for inputs the native kernel does not take (CPU tensors, fp64, bf16, ...):
     the reference's elementwise formula (utils/quantizers.py:21-32, :41-52) as torch ops in
-    w's own dtype and device -- torch's own log2 / round decide, so the result is the
-    reference's bit for bit in every dtype.  Product code for those inputs only; fp32 HIP
-    tensors always take the native kernel."""
+    w's own dtype and device, so torch's log2 / round of that device decide.  On CPU tensors
+    that is the reference's own arithmetic: bit for bit its outputs in every dtype
+    (tests/test_restated_quantizer.py).  On HIP tensors the device's log2 can land on the other
+    side of a rounding tie than the CPU's near k + 1/2: up to 0.5 % of the elements one
+    exponent step off the reference's CPU result (tests/test_gpu_quantizer.py, what the
+    reference's formula itself does on a GPU).  Product code for those inputs only; fp32 HIP
+    tensors always take the native, bit-exact kernel."""
     scale = torch.max(torch.abs(w))  # (raises for an empty tensor, as the reference does)
     a = (w / scale).abs()
     t = torch.log2(a / 1.5) + 0.5 if mode == "po2+" else torch.log2(a)
@@ -483,16 +490,29 @@ def chain_supported(x_shape, n_layers, bits=4, mode="po2", fsr=1):
 
 def qconv2d_chain(x, weights, bits=4, mode="po2", fsr=1, biases=None, post_scales=None, post_shifts=None,
                   acts=None, res_from=None):
-    """len(weights) quantized 3x3 / stride-1 / pad-1 C -> C convs in ONE launch (po2q_qconv2d_chain_f32):
+    """len(weights) quantized 3x3 / stride-1 / pad-1 C -> C convs in ONE launch (po2q_qconv2d_chain_f32,
+    torch.ops.po2q.qconv2d_chain):
         a_0 = x;  a_{l+1} = act_l((conv(a_l, Q(w_l)) + bias_l) * post_scale_l + post_shift_l
                                   (+ a_{res_from[l]}));   returns a_L
     -- the stride-1 run of a ResNet stage at CIFAR size, QuantizedConv2d.forward after
     QuantizedConv2d.forward as models/resnet.py:55-71 chains them (BN folded into the affine, the
-    identity shortcut as res_from = the block's first layer).  None entries / lists: skipped."""
-    _require_hip_f32(x, "input")
+    identity shortcut as res_from = the block's first layer).  A None list: none for every layer;
+    a None entry: none for that layer; a list must have one entry per weight."""
     n = len(weights)
+    for what, lst in (("biases", biases), ("post_scales", post_scales), ("post_shifts", post_shifts),
+                      ("acts", acts), ("res_from", res_from)):
+        if lst is not None and len(lst) != n:
+            raise Po2qError("po2q: chain: %s must have one entry per weight (%d), got %d" % (what, n, len(lst)))
+    _require_hip_f32(x, "input")
     for i, w in enumerate(weights):
         _require_hip_f32(w, "weight %d" % i)
+    O = ops()
+    if O is not None:
+        return _op_call(O.qconv2d_chain, x, list(weights), int(bits), MODES[mode], int(fsr),
+                        list(biases) if biases is not None else [], list(post_scales) if post_scales is not None else [],
+                        list(post_shifts) if post_shifts is not None else [],
+                        [ACTS[a] for a in acts] if acts is not None else [],
+                        [-1 if r is None else int(r) for r in res_from] if res_from is not None else [])
     L = load()
     xc = x.contiguous()
     N, C, H, W = (int(v) for v in xc.shape)
@@ -533,6 +553,50 @@ def qconv2d_chain(x, weights, bits=4, mode="po2", fsr=1, biases=None, post_scale
     return y
 
 
+def _layer_geometry(x_shape, stride, padding, dilation, groups):
+    """The 11 geometry ints of qconv2d_pack_batch for one layer: N C H W, stride, padding, dilation, groups."""
+    N, C, H, W = (int(v) for v in x_shape)
+    return [N, C, H, W, *_pair(stride), *_pair(padding), *_pair(dilation), int(groups)]
+
+
+def pack_batch(layers, bits=4, mode="po2", fsr=1, precision="auto"):
+    """The weight quantize + pack of several QuantizedConv2d.forward calls (models/quantized_conv.py:35)
+    as batched launches (torch.ops.po2q.qconv2d_pack_batch -> po2q_qconv2d_plan_pack_batch): layers =
+    [(w, x_shape, stride, padding, dilation, groups)], all with this (bits, mode, fsr, precision).
+    Returns one workspace per layer for qconv2d_packed (an empty one where the layer's kernel stages
+    its own weight).  Every layer runs the plan qconv2d() would run for it (the tuned / saved one)."""
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: pack_batch needs the operator library (PO2Q_LIB selects another build)")
+    mode_id, prec = MODES[mode], PRECISIONS[precision]
+    geom, plans_, ws = [], [], []
+    for w, x_shape, stride, padding, dilation, groups in layers:
+        _require_hip_f32(w, "weight")
+        g = _layer_geometry(x_shape, stride, padding, dilation, groups)
+        geom += g
+        K, _, R, S = w.shape
+        key = tuple(g[:4]) + (int(K), int(R), int(S)) + tuple(g[4:]) + (int(bits), int(fsr), mode_id, prec)
+        saved = _saved_plan(key)
+        plans_.append(-1 if saved is None else int(saved))
+        ws.append(w)
+    return _op_call(O.qconv2d_pack_batch, ws, geom, int(bits), mode_id, int(fsr), prec, plans_)
+
+
+def qconv2d_packed(x, w, workspace, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
+                   precision="auto", post_scale=None, post_shift=None, residual=None, act="none"):
+    """qconv2d_fused from a workspace pack_batch filled (the conv and its epilogue only; the weight
+    was quantized + packed by the batched launch).  Bit for bit qconv2d_fused's result."""
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: qconv2d_packed needs the operator library (PO2Q_LIB selects another build)")
+    xc, wc, bc, args, yshape = _conv_geometry(x, w, bias, stride, padding, dilation, groups)
+    key = args + (int(bits), int(fsr), MODES[mode], PRECISIONS[precision])
+    saved = _saved_plan(key)
+    return _op_call(O.qconv2d_packed, xc, wc, workspace, bc, list(args[7:9]), list(args[9:11]), list(args[11:13]),
+                    args[13], int(bits), MODES[mode], int(fsr), PRECISIONS[precision], -1 if saved is None else int(saved),
+                    post_scale, post_shift, residual, ACTS[act])
+
+
 class PackedConvs:
     """Several QuantizedConv2d forwards (models/quantized_conv.py:32-38) with their weight
     quantize + pack as ONE batched launch (po2q_qconv2d_plan_pack_batch) and each conv from its
@@ -543,17 +607,20 @@ class PackedConvs:
     plans are resolved once here, so create it after the shapes were autotuned.  Call pack()
     once per forward (after any weight update), then conv(i, x) for each layer.
 
-    The weights are held by reference and read at every pack(): they must be contiguous and
-    updated in place (an optimizer step, copy_); a module whose .weight is replaced by another
-    tensor (.to(), reassignment) needs a new PackedConvs.  pack() checks that every held
-    tensor still has the storage it had here."""
+    w is a weight tensor or a module with a .weight (a QuantizedConv2d).  A module's .weight is
+    re-read at every pack() and conv(), so a replaced parameter (load_state_dict(assign=True),
+    module.weight = ..., .to()) is picked up; a tensor is held by reference and must be updated in
+    place (pack() raises if its storage changed)."""
 
     def __init__(self, specs, bits=4, mode="po2", fsr=1):
         L = load()
         self._L = L
         self.bits, self.mode, self.fsr = int(bits), MODES[mode], int(fsr)
         self.plans, self.ws, self.w, self.xshape, self.yshape = [], [], [], [], []
+        self.src = []
         for x_shape, w, stride, padding in specs:
+            self.src.append(w)
+            w = w.weight if hasattr(w, "weight") and not isinstance(w, torch.Tensor) else w
             _require_hip_f32(w, "weight")
             if not w.is_contiguous():
                 raise Po2qError("po2q: PackedConvs needs contiguous weights (it reads them in place at every pack)")
@@ -580,11 +647,30 @@ class PackedConvs:
         self._sa = (ctypes.c_void_p * n)(*[t.data_ptr() for t in self.ws])
         self._ba = (ctypes.c_size_t * n)(*[t.numel() for t in self.ws])
 
+    def _refresh(self):
+        """Re-read the modules' weights; returns False if nothing changed."""
+        changed = False
+        for i, src in enumerate(self.src):
+            if isinstance(src, torch.Tensor):
+                if src.data_ptr() != self._wptr[i]:
+                    raise Po2qError("po2q: PackedConvs weight %d changed storage since construction "
+                                    "(set_() / resize); pass the module instead, or build a new PackedConvs" % i)
+                continue
+            w = src.weight
+            if w is self.w[i] and w.data_ptr() == self._wptr[i]:
+                continue
+            _require_hip_f32(w, "weight")
+            if tuple(w.shape) != tuple(self.w[i].shape) or w.device != self.w[i].device or not w.is_contiguous():
+                raise Po2qError("po2q: PackedConvs module %d's weight changed shape / device / layout; build a new "
+                                "PackedConvs" % i)
+            self.w[i] = w
+            self._wptr[i] = w.data_ptr()
+            self._wa[i] = w.data_ptr()
+            changed = True
+        return changed
+
     def pack(self):
-        for i, w in enumerate(self.w):
-            if w.data_ptr() != self._wptr[i]:
-                raise Po2qError("po2q: PackedConvs weight %d changed storage since construction "
-                                "(set_() / resize); build a new PackedConvs" % i)
+        self._refresh()
         if self._n:
             _check(self._L.po2q_qconv2d_plan_pack_batch(self._n, self._pa, self._wa, self._sa, self._ba,
                                                         _stream(self.w[0].device)))

@@ -161,6 +161,15 @@ static inline void clamp_window_host(int bits, int fsr, int& lo, int& hi) {
     hi = fsr - 1;
 }
 
+// Whether run_plan's RUN_PACK phase enqueues anything for plan p: not for the plans that
+// stage their weight in-kernel (bf16x3 with fused staging) or read it as given (fp32 stems /
+// pointwise of mode none).
+static bool plan_packs_weight(const ConvPlan& p, int /*mode*/) {
+    if (p.kind == KIND_DIRECT_F32 || p.kind == KIND_PW_F32) return false;
+    if (is_bf16x3_kind(p.kind) && p.fp) return false;
+    return true;
+}
+
 // phases of run_plan: the weight quantize + pack into the workspace, the conv from it
 enum { RUN_PACK = 1, RUN_CONV = 2, RUN_ALL = 3 };
 
@@ -182,6 +191,10 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     int st;
     if (p.kind == KIND_DIRECT_F32 || p.kind == KIND_PW_F32) {  // mode none: the weight as given, no pack
         if (!(phases & RUN_CONV)) return PO2Q_OK;
+        if (!w) {
+            set_error("po2q: this fp32 plan reads the weight as given: it needs w (no packed form)");
+            return PO2Q_ERR_INVALID;
+        }
         return hip_status(launch_conv_f32s(p, x, w, bias, y, e.ps, e.pb, e.res, e.act, s), "conv launch");
     }
     if ((phases & RUN_PACK) && L.nparts > 0) {
@@ -425,15 +438,20 @@ static int pick_split_plan(ConvPlan& p, int index, int64_t N, int64_t C, int64_t
                            int64_t groups, int mode, int bits, int fsr, int flags) {
     const int st = pick_plan(p, index, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags);
     if (st) return st;
-    if (p.kind == KIND_BF16X3_ROWS && p.vrx == 5) {
-        // the stride-2 full-row kernel only exists with fused staging (it has no pre-packed
-        // twin): take the first candidate that reads a packed weight instead
+    // plans with no packed form: the stride-2 full-row kernel only exists with fused staging,
+    // and the unquantized fp32 kernels (direct stem, pointwise) read the weight as given and
+    // pack nothing, so a split enqueue would run them without a weight.  Take the first
+    // candidate that reads a packed weight instead (for mode none: the fp32 MFMA kernel).
+    auto unpacked = [](const ConvPlan& c) {
+        return (c.kind == KIND_BF16X3_ROWS && c.vrx == 5) || c.kind == KIND_DIRECT_F32 || c.kind == KIND_PW_F32;
+    };
+    if (unpacked(p)) {
         std::vector<ConvPlan> cands;
         if (!plan_candidates(cands, N, C, H, W, K, R, S, sh, sw, ph, pw, dh, dw, groups, mode, bits, fsr, flags))
             return PO2Q_ERR_INVALID;
         bool found = false;
         for (const ConvPlan& c : cands)
-            if (!c.fp && !(c.kind == KIND_BF16X3_ROWS && c.vrx == 5)) {
+            if (!c.fp && !unpacked(c)) {
                 p = c;
                 found = true;
                 break;
@@ -565,11 +583,7 @@ int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, cons
         return PO2Q_ERR_INVALID;
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    std::vector<const ConvPlan*> bp;
-    std::vector<const float*> bw;
-    std::vector<uint16_t*> bpk;
-    std::vector<float*> bsc;
-    int bits = 0, fsr = 0, mode = 0;
+    std::vector<PackReq> reqs;
     for (int i = 0; i < n; ++i) {
         const po2q_conv_plan* h = plans[i];
         if (!h || !w[i] || !workspace[i]) {
@@ -582,26 +596,27 @@ int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, cons
             set_error("po2q: pack batch: workspace too small (need " + std::to_string(L.total) + " bytes)");
             return PO2Q_ERR_WORKSPACE;
         }
-        const bool x3 = is_bf16x3_kind(p.kind);
-        if (x3 && p.fp) continue;  // the conv stages its own weight
-        const bool batchable = x3 && L.nparts == 0 && (bp.empty() || (h->bits == bits && h->fsr == fsr && h->mode == mode));
-        if (!batchable) {  // its own pack launch(es), as po2q_qconv2d_pack_f32
+        if (!plan_packs_weight(p, h->mode)) continue;  // the conv stages its own weight / reads it as given
+        if (!pack_batchable(p, h->mode) || L.nparts > 0) {  // its own pack launch(es), as po2q_qconv2d_pack_f32
             const int st = run_plan(p, nullptr, w[i], nullptr, nullptr, h->bits, h->fsr, h->mode, workspace[i],
                                     workspace_bytes[i], s, ConvEpi{nullptr, nullptr, nullptr, 0}, RUN_PACK);
             if (st) return st;
             continue;
         }
-        bits = h->bits; fsr = h->fsr; mode = h->mode;
         char* ws = reinterpret_cast<char*>(workspace[i]);
-        bp.push_back(&p);
-        bw.push_back(w[i]);
-        bpk.push_back(reinterpret_cast<uint16_t*>(ws + L.packed_off));
-        bsc.push_back(reinterpret_cast<float*>(ws + L.scale_off));
+        reqs.push_back(PackReq{&p, w[i], ws + L.packed_off, reinterpret_cast<float*>(ws + L.scale_off), h->bits, h->fsr,
+                               h->mode});
     }
-    if (bp.empty()) return PO2Q_OK;
-    return hip_status(launch_pack_bf16x3_batch((int)bp.size(), bp.data(), bw.data(), bpk.data(), bsc.data(), bits, fsr,
-                                               mode, s),
-                      "batched weight pack launch");
+    if (reqs.empty()) return PO2Q_OK;
+    return hip_status(launch_pack_batch((int)reqs.size(), reqs.data(), s), "batched weight pack launch");
+}
+
+int po2q_qconv2d_plan_packs_weight(const po2q_conv_plan* plan) {
+    if (!plan) {
+        po2q::set_error("po2q: null plan");
+        return -PO2Q_ERR_INVALID;
+    }
+    return plan_packs_weight(plan->p, plan->mode) ? 1 : 0;
 }
 
 int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, const float* w, const float* bias,

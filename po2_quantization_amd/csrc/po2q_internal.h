@@ -153,7 +153,21 @@ hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned*
                               int bits, int fsr, int mode, uint16_t* packed, float* scale_out,
                               hipStream_t s);
 
-// The same for n weight tensors (plans[i] bf16x3 kinds, fused absmax) in ceil(n / 24) launches.
+// One weight tensor of a batched pack: plan (a bf16x3 kind, or KIND_DEPTHWISE: the plain
+// quantized fp32 copy), weight, destination (bf16 fragments / fp32 copy), scale slot (bf16x3).
+struct PackReq {
+    const ConvPlan* plan;
+    const float* w;
+    void* packed;
+    float* scale;
+    int bits, fsr, mode;
+};
+// whether a plan's weight staging can join a batched pack (quantized, fused absmax size,
+// bf16x3 or depthwise kind)
+bool pack_batchable(const ConvPlan& p, int mode);
+// n weight tensors (pack_batchable plans, each with its own bits / fsr / mode) in ceil(n / 24) launches
+hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s);
+// The same for n bf16x3 weight tensors with one (bits, fsr, mode).
 hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
                                     uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
                                     hipStream_t s);

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "po2q_internal.h"
 #include "po2q_quant_dev.h"
@@ -173,8 +174,38 @@ struct PackX3 {
 // finishes in one or two rounds of independent loads per thread.
 constexpr int kPackThreads = 1024;
 
+// max|w| bits of a small (L2-resident, < 2^20 elements) weight tensor, reduced by every
+// thread of the block (kPackThreads threads): the pack kernels' fused absmax.
+__device__ __forceinline__ unsigned fused_absmax_bits(const float* __restrict__ w, int64_t n) {
+    unsigned m = 0u;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(w) & 15u) == 0);
+    int i0 = 0;  // the planner keeps fused weights below 2^20 elements
+    if (aligned) {
+        const int n4 = (int)(n >> 2);
+        const float4* w4 = reinterpret_cast<const float4*>(w);
+        constexpr int U = 8;  // independent loads in flight per thread
+        for (int i = threadIdx.x; i < n4; i += U * kPackThreads) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = i + u * kPackThreads;
+                v[u] = (k < n4) ? w4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned a = __float_as_uint(v[u].x) & 0x7fffffffu, b = __float_as_uint(v[u].y) & 0x7fffffffu;
+                const unsigned c = __float_as_uint(v[u].z) & 0x7fffffffu, d = __float_as_uint(v[u].w) & 0x7fffffffu;
+                m = max(m, max(max(a, b), max(c, d)));
+            }
+        }
+        i0 = n4 << 2;
+    }
+    for (int i = i0 + threadIdx.x; i < (int)n; i += kPackThreads) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+    return m;
+}
+
 // The pack of one weight tensor by block `bid` of `nb` (pack_bf16x3_kernel: one tensor per
-// launch; pack_bf16x3_batch_kernel: one tensor per blockIdx.y).
+// launch; pack_batch_kernel: one tensor per blockIdx.y).
 __device__ __forceinline__ void pack_bf16x3_body(const float* __restrict__ w, int64_t n,
                                                  const unsigned* __restrict__ partial, int nparts, int lo, int hi,
                                                  int mode, const PackX3& pg, uint16_t* __restrict__ packed,
@@ -186,29 +217,7 @@ __device__ __forceinline__ void pack_bf16x3_body(const float* __restrict__ w, in
     if (nparts > 0) {
         for (int i = threadIdx.x; i < nparts; i += kPackThreads) m = max(m, partial[i]);
     } else {  // fused absmax: every block reduces the whole (small, L2-resident) weight tensor
-        const bool aligned = ((reinterpret_cast<uintptr_t>(w) & 15u) == 0);
-        int i0 = 0;  // the planner keeps fused weights below 2^20 elements
-        if (aligned) {
-            const int n4 = (int)(n >> 2);
-            const float4* w4 = reinterpret_cast<const float4*>(w);
-            constexpr int U = 8;  // independent loads in flight per thread
-            for (int i = threadIdx.x; i < n4; i += U * kPackThreads) {
-                float4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = i + u * kPackThreads;
-                    v[u] = (k < n4) ? w4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const unsigned a = __float_as_uint(v[u].x) & 0x7fffffffu, b = __float_as_uint(v[u].y) & 0x7fffffffu;
-                    const unsigned c = __float_as_uint(v[u].z) & 0x7fffffffu, d = __float_as_uint(v[u].w) & 0x7fffffffu;
-                    m = max(m, max(max(a, b), max(c, d)));
-                }
-            }
-            i0 = n4 << 2;
-        }
-        for (int i = i0 + threadIdx.x; i < (int)n; i += kPackThreads) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+        m = fused_absmax_bits(w, n);
     }
     m = block_max_u32<kPackThreads / 64>(m, red);
     const float scale = __uint_as_float(m);
@@ -286,24 +295,36 @@ __global__ __launch_bounds__(kPackThreads) void pack_bf16x3_kernel(const float* 
 }
 
 // Up to kPackBatch weight tensors quantized + packed in one launch (blockIdx.y = tensor):
-// the per-layer pack launches of a whole forward become ceil(n / kPackBatch) launches.
+// the per-layer pack launches of a whole forward become ceil(n / kPackBatch) launches.  A job
+// is either the bf16x3 B-fragment pack of an MFMA plan (plain == 0) or the plain quantized
+// fp32 copy [K][1][R][S] a depthwise plan reads (plain == 1, quantize_plain_fused_kernel's work).
 struct PackJob {
     const float* w;
-    uint16_t* packed;
+    void* packed;
     float* scale;
     int64_t n;
-    int lo, hi, mode, nb;
+    int lo, hi, mode, nb, plain;
     PackX3 pg;
 };
-constexpr int kPackBatch = 24;  // 24 x 96-byte jobs: 2.3 KB of kernel arguments
+constexpr int kPackBatch = 24;  // 24 x 104-byte jobs: 2.5 KB of kernel arguments
 struct PackBatch {
     PackJob job[kPackBatch];
 };
 
-__global__ __launch_bounds__(kPackThreads) void pack_bf16x3_batch_kernel(PackBatch B) {
+__global__ __launch_bounds__(kPackThreads) void pack_batch_kernel(PackBatch B) {
     const PackJob& j = B.job[blockIdx.y];
     if ((int)blockIdx.x >= j.nb) return;  // block-uniform
-    pack_bf16x3_body(j.w, j.n, nullptr, 0, j.lo, j.hi, j.mode, j.pg, j.packed, j.scale, (int)blockIdx.x, j.nb);
+    if (j.plain) {
+        __shared__ unsigned red[kPackThreads / 64];
+        const unsigned m = block_max_u32<kPackThreads / 64>(fused_absmax_bits(j.w, j.n), red);
+        const float scale = __uint_as_float(m);
+        float* out = reinterpret_cast<float*>(j.packed);
+        for (int i = blockIdx.x * kPackThreads + threadIdx.x; i < (int)j.n; i += j.nb * kPackThreads)
+            out[i] = quantize_elem(j.w[i], scale, j.mode, j.lo, j.hi);
+        return;
+    }
+    pack_bf16x3_body(j.w, j.n, nullptr, 0, j.lo, j.hi, j.mode, j.pg, reinterpret_cast<uint16_t*>(j.packed), j.scale,
+                     (int)blockIdx.x, j.nb);
 }
 
 static PackX3 pack_geom(const ConvPlan& p) {
@@ -320,32 +341,51 @@ static int pack_blocks(const PackX3& pg) {
     return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 32);
 }
 
-hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
-                                    uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
-                                    hipStream_t s) {
-    int lo, hi;
-    clamp_window(bits, fsr, lo, hi);
+bool pack_batchable(const ConvPlan& p, int mode) {
+    const int64_t n = (int64_t)p.K * p.Cg * p.R * p.S;
+    if (mode == 0 || n > kFusedAbsmaxMax) return false;
+    return is_bf16x3_kind(p.kind) || p.kind == KIND_DEPTHWISE;
+}
+
+hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s) {
     for (int i0 = 0; i0 < n; i0 += kPackBatch) {
         PackBatch B;
         const int m = std::min(kPackBatch, n - i0);
         int nbmax = 1;
         for (int i = 0; i < m; ++i) {
-            const ConvPlan& p = *plans[i0 + i];
+            const PackReq& r = reqs[i0 + i];
+            const ConvPlan& p = *r.plan;
             PackJob& j = B.job[i];
-            j.w = w[i0 + i];
-            j.packed = packed[i0 + i];
-            j.scale = scale_out[i0 + i];
+            int lo, hi;
+            clamp_window(r.bits, r.fsr, lo, hi);
+            j.w = r.w;
+            j.packed = r.packed;
+            j.scale = r.scale;
             j.n = (int64_t)p.K * p.Cg * p.R * p.S;
-            j.lo = lo; j.hi = hi; j.mode = mode - 1;
-            j.pg = pack_geom(p);
-            j.nb = pack_blocks(j.pg);
+            j.lo = lo; j.hi = hi; j.mode = r.mode - 1;
+            j.plain = p.kind == KIND_DEPTHWISE ? 1 : 0;
+            if (j.plain) {
+                j.pg = PackX3{};
+                j.nb = (int)std::min<int64_t>(8, (j.n + kPackThreads * 4 - 1) / (kPackThreads * 4));
+            } else {
+                j.pg = pack_geom(p);
+                j.nb = pack_blocks(j.pg);
+            }
             nbmax = std::max(nbmax, j.nb);
         }
-        hipLaunchKernelGGL(pack_bf16x3_batch_kernel, dim3((unsigned)nbmax, (unsigned)m), dim3(kPackThreads), 0, s, B);
+        hipLaunchKernelGGL(pack_batch_kernel, dim3((unsigned)nbmax, (unsigned)m), dim3(kPackThreads), 0, s, B);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,
+                                    uint16_t* const* packed, float* const* scale_out, int bits, int fsr, int mode,
+                                    hipStream_t s) {
+    std::vector<PackReq> reqs((size_t)n);
+    for (int i = 0; i < n; ++i) reqs[i] = PackReq{plans[i], w[i], packed[i], scale_out[i], bits, fsr, mode};
+    return launch_pack_batch(n, reqs.data(), s);
 }
 
 hipError_t launch_pack_bf16x3(const ConvPlan& p, const float* w, const unsigned* partial, int nparts, int bits,

@@ -16,6 +16,12 @@
 //   po2q::conv_wgrad     the QAT backward's weight gradient (train.py:79-91 loss.backward();
 //                        STE, utils/quantizers.py:34-36), dense and depthwise
 //   po2q::dilate         zero insertion for the strided layers' input gradient
+//   po2q::qconv2d_chain  a stage's stride-1 run of C -> C 3x3 qconvs (BasicBlocks at CIFAR size)
+//                        in one launch (resnet.py:55-71 chained by :131-143)
+//   po2q::qconv2d_pack_batch / po2q::qconv2d_packed
+//                        the weight quantize of every QuantizedConv2d.forward of a model forward
+//                        (quantized_conv.py:35) as batched launches, then each conv (+ epilogue)
+//                        from its packed workspace
 // Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
 // Errors are TORCH_CHECK -> RuntimeError, as F.conv2d raises for bad arguments.
 #include <ATen/ATen.h>
@@ -140,6 +146,26 @@ PlanEntry* plan_for(const Geometry& G, int64_t bits, int64_t fsr, int64_t mode, 
     e->tuned = autotune && plan < 0;
     PlanEntry* out = e.get();
     if (it != g_plans.end()) g_retired.push_back(std::move(it->second));
+    g_plans[k] = std::move(e);
+    return out;
+}
+
+// The plan qconv2d would run for this problem without autotuning (candidate `plan` >= 0, or
+// the tuned / heuristic one), created on first use; host-only (no device access).
+PlanEntry* plan_lookup(const std::array<int64_t, 14>& g, int64_t bits, int64_t fsr, int64_t mode, int64_t prec,
+                       int64_t plan, int64_t dev) {
+    Key k;
+    for (int i = 0; i < 14; ++i) k[i] = g[i];
+    k[14] = bits; k[15] = fsr; k[16] = mode; k[17] = prec; k[18] = plan; k[19] = dev;
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_plans.find(k);
+    if (it != g_plans.end()) return it->second.get();
+    auto e = std::make_unique<PlanEntry>();
+    const int st = po2q_qconv2d_plan_create(&e->plan, (int)plan, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8],
+                                            g[9], g[10], g[11], g[12], g[13], (int)bits, (int)fsr, (int)mode, (int)prec);
+    TORCH_CHECK(st == 0, last_error());
+    e->ws = po2q_qconv2d_plan_workspace_bytes(e->plan);
+    PlanEntry* out = e.get();
     g_plans[k] = std::move(e);
     return out;
 }
@@ -418,6 +444,191 @@ at::Tensor conv_wgrad_meta(const at::Tensor& x, const at::Tensor&, at::IntArrayR
     return at::empty(wshape, x.options());
 }
 
+// ---- a stage's stride-1 chain of C -> C 3x3 qconvs in one launch (po2q_qconv2d_chain_f32) ----
+// Empty epilogue / act / res_from lists mean "none"; otherwise each has one entry per weight.
+at::Tensor qconv2d_chain(const at::Tensor& x_, at::TensorList weights, int64_t bits, int64_t mode, int64_t fsr,
+                         const c10::List<c10::optional<at::Tensor>>& biases,
+                         const c10::List<c10::optional<at::Tensor>>& post_scales,
+                         const c10::List<c10::optional<at::Tensor>>& post_shifts, at::IntArrayRef acts,
+                         at::IntArrayRef res_from) {
+    check_hip_f32(x_, "input");
+    TORCH_CHECK(x_.dim() == 4, "po2q: chain: 4-D input");
+    const int64_t n = (int64_t)weights.size();
+    TORCH_CHECK(n >= 1 && n <= PO2Q_CHAIN_MAX_LAYERS, "po2q: chain: 1 to ", PO2Q_CHAIN_MAX_LAYERS, " layers, got ", n);
+    const int64_t C = x_.size(1);
+    for (auto [len, what] : {std::make_pair((int64_t)biases.size(), "biases"),
+                             std::make_pair((int64_t)post_scales.size(), "post_scales"),
+                             std::make_pair((int64_t)post_shifts.size(), "post_shifts"),
+                             std::make_pair((int64_t)acts.size(), "acts"),
+                             std::make_pair((int64_t)res_from.size(), "res_from")})
+        TORCH_CHECK(len == 0 || len == n, "po2q: chain: ", what, " must have one entry per weight (", n, ") or none, got ",
+                    len);
+    const DeviceGuard guard(x_.device());
+    const at::Tensor x = x_.contiguous();
+    std::vector<at::Tensor> keep;
+    std::vector<const float*> wp(n), bp(n, nullptr), sp(n, nullptr), hp(n, nullptr);
+    for (int64_t i = 0; i < n; ++i) {
+        check_hip_f32(weights[i], "chain weight");
+        TORCH_CHECK(weights[i].dim() == 4 && weights[i].size(0) == C && weights[i].size(1) == C &&
+                        weights[i].size(2) == 3 && weights[i].size(3) == 3,
+                    "po2q: chain weight ", i, " must be [", C, ", ", C, ", 3, 3], got ", weights[i].sizes());
+        TORCH_CHECK(weights[i].device() == x.device(), "po2q: chain: tensors on one device");
+        keep.push_back(weights[i].contiguous());
+        wp[i] = keep.back().data_ptr<float>();
+    }
+    auto vecs = [&](const c10::List<c10::optional<at::Tensor>>& l, std::vector<const float*>& out, const char* what) {
+        for (int64_t i = 0; i < (int64_t)l.size(); ++i) {
+            const c10::optional<at::Tensor> t = l.get(i);
+            if (!t.has_value()) continue;
+            check_vec(t, x, C, what);
+            keep.push_back(t->contiguous());
+            out[i] = keep.back().data_ptr<float>();
+        }
+    };
+    vecs(biases, bp, "chain bias");
+    vecs(post_scales, sp, "chain post_scale");
+    vecs(post_shifts, hp, "chain post_shift");
+    std::vector<int> av(acts.begin(), acts.end()), rv(res_from.begin(), res_from.end());
+    for (int a : av) TORCH_CHECK(a >= 0 && a <= 3, "po2q: chain: unknown activation ", a);
+    at::Tensor y = at::empty_like(x);
+    if (x.size(0) == 0) return y;
+    const size_t wsb = po2q_qconv2d_chain_workspace_bytes(x.size(0), C, x.size(2), x.size(3), (int)n);
+    TORCH_CHECK(wsb > 0, "po2q: chain: ", last_error());
+    at::Tensor ws = at::empty({(int64_t)wsb}, x.options().dtype(at::kByte));
+    const int st = po2q_qconv2d_chain_f32(x.data_ptr<float>(), wp.data(), biases.size() ? bp.data() : nullptr,
+                                          post_scales.size() ? sp.data() : nullptr,
+                                          post_shifts.size() ? hp.data() : nullptr, av.empty() ? nullptr : av.data(),
+                                          rv.empty() ? nullptr : rv.data(), (int)n, x.size(0), C, x.size(2), x.size(3),
+                                          (int)bits, (int)fsr, (int)mode, y.data_ptr<float>(), ws.data_ptr(), wsb,
+                                          stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return y;
+}
+
+at::Tensor qconv2d_chain_meta(const at::Tensor& x, at::TensorList, int64_t, int64_t, int64_t,
+                              const c10::List<c10::optional<at::Tensor>>&, const c10::List<c10::optional<at::Tensor>>&,
+                              const c10::List<c10::optional<at::Tensor>>&, at::IntArrayRef, at::IntArrayRef) {
+    return at::empty_like(x);
+}
+
+// ---- batched weight staging of a forward: pack once, run each conv from its workspace ----
+// geometry: 11 ints per layer (N C H W of the layer's input, stride h/w, padding h/w,
+// dilation h/w, groups); plans: the plan index per layer (-1: tuned / heuristic).  Returns
+// one byte workspace per layer (views of one allocation); a layer whose kernel stages its
+// weight itself (or reads it as given) gets an empty workspace and runs as qconv2d_fused.
+std::array<int64_t, 14> layer_geometry(at::IntArrayRef geometry, int64_t i, const at::Tensor& w) {
+    const int64_t* g = geometry.data() + 11 * i;
+    return {g[0], g[1], g[2], g[3], w.size(0), w.size(2), w.size(3), g[4], g[5], g[6], g[7], g[8], g[9], g[10]};
+}
+
+std::vector<at::Tensor> qconv2d_pack_batch(at::TensorList weights, at::IntArrayRef geometry, int64_t bits, int64_t mode,
+                                           int64_t fsr, int64_t prec, at::IntArrayRef plans) {
+    const int64_t n = (int64_t)weights.size();
+    TORCH_CHECK((int64_t)geometry.size() == 11 * n, "po2q: pack_batch: 11 geometry ints per weight");
+    TORCH_CHECK(plans.empty() || (int64_t)plans.size() == n, "po2q: pack_batch: one plan index per weight (or none)");
+    if (n == 0) return {};
+    check_hip_f32(weights[0], "weight");
+    const DeviceGuard guard(weights[0].device());
+    std::vector<PlanEntry*> es(n);
+    std::vector<at::Tensor> wc(n);
+    std::vector<int64_t> off(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        check_hip_f32(weights[i], "weight");
+        TORCH_CHECK(weights[i].dim() == 4 && weights[i].device() == weights[0].device(),
+                    "po2q: pack_batch: 4-D weights on one device");
+        wc[i] = weights[i].contiguous();
+        es[i] = plan_lookup(layer_geometry(geometry, i, wc[i]), bits, fsr, mode, prec, plans.empty() ? -1 : plans[i],
+                            weights[0].device().index());
+        const int pw = po2q_qconv2d_plan_packs_weight(es[i]->plan);
+        TORCH_CHECK(pw >= 0, last_error());
+        off[i + 1] = off[i] + (pw ? ((int64_t)es[i]->ws + 255) / 256 * 256 : 0);
+    }
+    at::Tensor all = at::empty({std::max<int64_t>(off[n], 256)}, weights[0].options().dtype(at::kByte));
+    std::vector<at::Tensor> out(n);
+    std::vector<const po2q_conv_plan*> hp;
+    std::vector<const float*> wp;
+    std::vector<void*> sp;
+    std::vector<size_t> bp;
+    for (int64_t i = 0; i < n; ++i) {
+        out[i] = all.narrow(0, off[i], off[i + 1] - off[i]);
+        if (off[i + 1] == off[i]) continue;
+        hp.push_back(es[i]->plan);
+        wp.push_back(wc[i].data_ptr<float>());
+        sp.push_back(out[i].data_ptr());
+        bp.push_back(es[i]->ws);
+    }
+    if (!hp.empty()) {
+        const int st = po2q_qconv2d_plan_pack_batch((int)hp.size(), hp.data(), wp.data(), sp.data(), bp.data(),
+                                                    stream_of(weights[0]));
+        TORCH_CHECK(st == 0, last_error());
+    }
+    return out;
+}
+
+std::vector<at::Tensor> qconv2d_pack_batch_meta(at::TensorList weights, at::IntArrayRef geometry, int64_t bits,
+                                                int64_t mode, int64_t fsr, int64_t prec, at::IntArrayRef plans) {
+    const int64_t n = (int64_t)weights.size();
+    TORCH_CHECK((int64_t)geometry.size() == 11 * n && (plans.empty() || (int64_t)plans.size() == n),
+                "po2q: pack_batch: bad lists");
+    std::vector<at::Tensor> out;
+    for (int64_t i = 0; i < n; ++i) {
+        PlanEntry* e = plan_lookup(layer_geometry(geometry, i, weights[i]), bits, fsr, mode, prec,
+                                   plans.empty() ? -1 : plans[i], -1);
+        const int pw = po2q_qconv2d_plan_packs_weight(e->plan);
+        out.push_back(at::empty({pw > 0 ? (int64_t)e->ws : 0}, weights[i].options().dtype(at::kByte)));
+    }
+    return out;
+}
+
+at::Tensor qconv2d_packed(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& workspace,
+                          const c10::optional<at::Tensor>& bias_, at::IntArrayRef stride, at::IntArrayRef padding,
+                          at::IntArrayRef dilation, int64_t groups, int64_t bits, int64_t mode, int64_t fsr,
+                          int64_t prec, int64_t plan, const c10::optional<at::Tensor>& post_scale,
+                          const c10::optional<at::Tensor>& post_shift, const c10::optional<at::Tensor>& residual,
+                          int64_t act) {
+    if (workspace.numel() == 0)  // nothing was pre-packed: the kernel stages its own weight
+        return qconv2d_impl(x_, w_, bias_, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, 0,
+                            post_scale, post_shift, residual, act);
+    TORCH_CHECK(act >= 0 && act <= 3, "po2q: unknown activation ", act);
+    const Geometry G = conv_geometry(x_, w_, bias_, stride, padding, dilation, groups);
+    TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kByte && workspace.is_contiguous() &&
+                    workspace.device() == x_.device(),
+                "po2q: packed: the workspace must be a contiguous uint8 tensor on the input's device");
+    const DeviceGuard guard(x_.device());
+    PlanEntry* e = plan_lookup(G.g, bits, fsr, mode, prec, plan, x_.device().index());
+    TORCH_CHECK((size_t)workspace.numel() >= e->ws,
+                "po2q: packed: workspace of ", workspace.numel(), " bytes, the plan needs ", e->ws,
+                " (pack it with qconv2d_pack_batch for this geometry)");
+    const at::Tensor x = x_.contiguous(), w = w_.contiguous();
+    c10::optional<at::Tensor> bias, ps, pb, res;
+    if (bias_.has_value()) bias = bias_->contiguous();
+    check_vec(post_scale, x, G.yshape[1], "post_scale");
+    check_vec(post_shift, x, G.yshape[1], "post_shift");
+    if (post_scale.has_value()) ps = post_scale->contiguous();
+    if (post_shift.has_value()) pb = post_shift->contiguous();
+    if (residual.has_value()) {
+        check_hip_f32(*residual, "residual");
+        TORCH_CHECK(residual->device() == x.device() && residual->sizes() == at::IntArrayRef(G.yshape),
+                    "po2q: residual shape ", residual->sizes(), " does not match the output ", at::IntArrayRef(G.yshape));
+        res = residual->contiguous();
+    }
+    at::Tensor y = at::empty(G.yshape, x.options());
+    if (G.yshape[0] == 0) return y;
+    const int st = po2q_qconv2d_plan_run_packed(e->plan, x.data_ptr<float>(), w.data_ptr<float>(), opt_ptr(bias),
+                                                y.data_ptr<float>(), opt_ptr(ps), opt_ptr(pb), opt_ptr(res), (int)act,
+                                                workspace.data_ptr(), (size_t)workspace.numel(), stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return y;
+}
+
+at::Tensor qconv2d_packed_meta(const at::Tensor& x, const at::Tensor& w, const at::Tensor&,
+                               const c10::optional<at::Tensor>& bias, at::IntArrayRef stride, at::IntArrayRef padding,
+                               at::IntArrayRef dilation, int64_t groups, int64_t bits, int64_t mode, int64_t fsr,
+                               int64_t prec, int64_t plan, const c10::optional<at::Tensor>&,
+                               const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, int64_t) {
+    return qconv2d_meta(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, 0);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(po2q, m) {
@@ -437,6 +648,13 @@ TORCH_LIBRARY(po2q, m) {
     m.def("qconv2d_s2ds(Tensor x, Tensor w, Tensor wds, int bits, int mode, int fsr=1, Tensor? post_scale=None, "
           "Tensor? post_shift=None, int act=0, Tensor? post_scale_ds=None, Tensor? post_shift_ds=None) "
           "-> (Tensor, Tensor)");
+    m.def("qconv2d_chain(Tensor x, Tensor[] weights, int bits, int mode, int fsr, Tensor?[] biases, "
+          "Tensor?[] post_scales, Tensor?[] post_shifts, int[] acts=[], int[] res_from=[]) -> Tensor");
+    m.def("qconv2d_pack_batch(Tensor[] weights, int[] geometry, int bits, int mode, int fsr=1, int precision=0, "
+          "int[] plans=[]) -> Tensor[]");
+    m.def("qconv2d_packed(Tensor x, Tensor w, Tensor workspace, Tensor? bias, int[2] stride, int[2] padding, "
+          "int[2] dilation, int groups, int bits, int mode, int fsr=1, int precision=0, int plan=-1, "
+          "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
@@ -448,6 +666,9 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("dilate", &dilate);
     m.impl("qconv2d_pair", &qconv2d_pair);
     m.impl("qconv2d_s2ds", &qconv2d_s2ds);
+    m.impl("qconv2d_chain", &qconv2d_chain);
+    m.impl("qconv2d_pack_batch", &qconv2d_pack_batch);
+    m.impl("qconv2d_packed", &qconv2d_packed);
 }
 
 TORCH_LIBRARY_IMPL(po2q, Meta, m) {
@@ -459,4 +680,7 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("dilate", &dilate_meta);
     m.impl("qconv2d_pair", &qconv2d_pair_meta);
     m.impl("qconv2d_s2ds", &qconv2d_s2ds_meta);
+    m.impl("qconv2d_chain", &qconv2d_chain_meta);
+    m.impl("qconv2d_pack_batch", &qconv2d_pack_batch_meta);
+    m.impl("qconv2d_packed", &qconv2d_packed_meta);
 }

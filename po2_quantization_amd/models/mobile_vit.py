@@ -26,7 +26,8 @@ from typing import Any, Callable, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .quantized_conv import QuantizedConv2d, can_fuse, fusable_sequence, run_fused_sequence, run_sequence
+from .quantized_conv import (QuantizedConv2d, batched_packs, can_fuse, fusable_sequence, run_fused_sequence,
+                             run_sequence)
 
 
 def quantized_conv_1x1_bn(inp, oup, quantize_fn=None, bits=4):
@@ -208,12 +209,13 @@ class MobileViT(nn.Module):
                                        nn.Linear(c[-1], num_classes, bias=False))
 
     def forward(self, x):
-        x = run_sequence(self.conv1, x)  # unquantized stem: one native fp32 call in eval
-        for blk in self.stem:
-            x = blk(x)
-        for mv2, vit in self.trunk:
-            x = vit(mv2(x))
-        x = run_sequence(self.to_logits[0], x)
+        with batched_packs(self, x):  # eval: the single-conv layers' weight packs as batched launches
+            x = run_sequence(self.conv1, x)  # unquantized stem: one native fp32 call in eval
+            for blk in self.stem:
+                x = blk(x)
+            for mv2, vit in self.trunk:
+                x = vit(mv2(x))
+            x = run_sequence(self.to_logits[0], x)
         for m in list(self.to_logits)[1:]:
             x = m(x)
         return x

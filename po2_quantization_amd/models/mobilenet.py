@@ -22,7 +22,8 @@ from typing import Any, Callable, Optional
 
 import torch.nn as nn
 
-from .quantized_conv import QuantizedConv2d, can_fuse, fusable_sequence, run_fused_sequence, run_sequence
+from .quantized_conv import (QuantizedConv2d, batched_packs, can_fuse, fusable_sequence, run_fused_sequence,
+                             run_sequence)
 
 # (expand ratio t, output channels c, repeats n, first stride s) -- mobilenet.py:153-161
 MOBILENET_V2_SETTINGS = ((1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2),
@@ -105,9 +106,10 @@ class MobileNet(nn.Module):
         self._initialize_weights()
 
     def forward(self, x):
-        for m in self.features:  # the unquantized stem (features[0]) natively fused in eval too
-            x = run_sequence(m, x) if isinstance(m, nn.Sequential) else m(x)
-        x = self.avgpool(run_sequence(self.conv, x))
+        with batched_packs(self, x):  # eval: every layer's weight pack as batched launches
+            for m in self.features:  # the unquantized stem (features[0]) natively fused in eval too
+                x = run_sequence(m, x) if isinstance(m, nn.Sequential) else m(x)
+            x = self.avgpool(run_sequence(self.conv, x))
         return self.classifier(x.flatten(1))
 
     def _initialize_weights(self):

@@ -24,6 +24,8 @@ into a per-channel affine), the activation and the residual add, in one native c
 built and the BatchNorms are in eval mode; otherwise they run the reference's module
 sequence unchanged.
 """
+import contextlib
+
 import torch
 import torch.nn as nn
 
@@ -154,6 +156,54 @@ def can_fuse(*mods):
     return True
 
 
+# Batched weight staging of an eval forward (the reference quantizes each layer's weight inside
+# its own forward, quantized_conv.py:35).  Layers whose kernel reads a pre-packed weight (the
+# single-conv row / pointwise / depthwise plans; the pair, stride-2, chain and fused-staging
+# kernels quantize their weights themselves) get their quantize + pack from ONE batched launch
+# per 24 layers at the start of the forward (torch.ops.po2q.qconv2d_pack_batch), then run from
+# the packed workspace (qconv2d_packed): the same plans and results, bit for bit, with every
+# weight still re-quantized in every forward.  The first forward of a model at an input shape
+# records which layers do that and at which shapes; later forwards at that shape pack them
+# up front.  False: every layer packs its own weight (A/B runs).
+BATCHED_PACKS = True
+_packs = None  # the active forward's _ForwardPacks (None outside batched_packs)
+
+
+class _ForwardPacks:
+    def __init__(self, layers):
+        self.recording = [] if layers is None else None
+        self.ws = {}
+        if layers is None:
+            return
+        groups = {}
+        for m, g, conf in layers:
+            groups.setdefault(conf, []).append((m, g))
+        for (bits, mode, prec), items in groups.items():
+            ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g in items], bits, mode, 1, prec)
+            for (m, g), w in zip(items, ws):
+                self.ws[id(m)] = (g, m.weight, w)
+
+
+@contextlib.contextmanager
+def batched_packs(model, x):
+    """Run a model's eval forward with its single-conv layers' weight packs batched (BATCHED_PACKS)."""
+    global _packs
+    if (not BATCHED_PACKS or _packs is not None or torch.is_grad_enabled() or model.training
+            or not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32)):
+        yield
+        return
+    key = (tuple(x.shape), x.device)
+    rec = model.__dict__.setdefault("_po2q_packs", {})
+    sess = _ForwardPacks(rec.get(key))
+    _packs = sess
+    try:
+        yield
+    finally:
+        _packs = None
+    if sess.recording is not None:
+        rec[key] = sess.recording
+
+
 class QuantizedConv2d(nn.Conv2d):
     # conv arithmetic of the native kernels: "auto" | "fp32" | "bf16x3"
     precision = "auto"
@@ -220,6 +270,17 @@ class QuantizedConv2d(nn.Conv2d):
             weight = self.quantize_fn.apply(self.weight, self.bits)
             mode = "none"
         ps, pb = fold_bn(bn) if bn is not None else (None, None)
+        sess = _packs
+        if sess is not None and mode != "none" and input.dim() == 4:
+            g = (tuple(input.shape), tuple(self.stride), tuple(self._padding(input)), tuple(self.dilation), self.groups)
+            if sess.recording is not None:
+                sess.recording.append((self, g, (self.bits, mode, self.precision)))
+            else:
+                hit = sess.ws.get(id(self))
+                if hit is not None and hit[0] == g and hit[1] is weight and hit[2].numel() > 0:
+                    return _lib.qconv2d_packed(input, weight, hit[2], self.bias, g[1], g[2], g[3], g[4], self.bits,
+                                               mode, 1, self.precision, post_scale=ps, post_shift=pb,
+                                               residual=residual, act=act or "none")
         return _lib.qconv2d_fused(input, weight, self.bias, self.stride, self._padding(input), self.dilation,
                                   self.groups, self.bits, mode, 1, self.precision, post_scale=ps, post_shift=pb,
                                   residual=residual, act=act or "none")

@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..utils.quantizers import NATIVE_MODES
-from .quantized_conv import QuantizedConv2d, can_fuse, fold_bn, plain_conv_fused, run_fused_sequence
+from .quantized_conv import QuantizedConv2d, batched_packs, can_fuse, fold_bn, plain_conv_fused, run_fused_sequence
 
 
 class BasicBlock(nn.Module):
@@ -143,13 +143,14 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        if can_fuse(self.bn1) and x.is_cuda and x.dtype == torch.float32:
-            # the unquantized stem conv + bn1 + relu (resnet.py:99-102, 191) as one native fp32 call
-            x = plain_conv_fused(self.conv1, x, bn=self.bn1, act="relu")
-        else:
-            x = self.relu(self.bn1(self.conv1(x)))
-        for layer in (self.layer1, self.layer2, self.layer3):
-            x = self._stage(layer, x)
+        with batched_packs(self, x):  # eval: the single-conv layers' weight packs as batched launches
+            if can_fuse(self.bn1) and x.is_cuda and x.dtype == torch.float32:
+                # the unquantized stem conv + bn1 + relu (resnet.py:99-102, 191) as one native fp32 call
+                x = plain_conv_fused(self.conv1, x, bn=self.bn1, act="relu")
+            else:
+                x = self.relu(self.bn1(self.conv1(x)))
+            for layer in (self.layer1, self.layer2, self.layer3):
+                x = self._stage(layer, x)
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
     def _stage(self, layer, x):

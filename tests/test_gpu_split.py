@@ -55,3 +55,24 @@ def test_split_stride2_transitions(shape, mode):
     sc.pack()
     y = sc.conv(x)
     assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 20, 24, 16, 3, 1, 1), (2, 3, 32, 32, 16, 3, 2, 1), (2, 32, 10, 12, 48, 1, 1, 0)],
+                         ids=["stem3x3", "stem3x3s2", "pw1x1"])
+def test_split_mode_none_unpacked_plans(shape):
+    """Mode none on the shapes whose heuristic plan is an fp32 kernel that reads the weight as
+    given (the 3-channel direct stem, the 1x1 pointwise GEMM): those have no packed form, so the
+    split enqueue must fall back to a plan that packs the weight (it launched with a
+    null weight).  Checked against the one-call form (a different kernel: normwise)."""
+    from tests._util import CONV_TOL
+
+    N, C, H, W, K, R, st, pad = shape
+    torch.manual_seed(sum(shape))
+    x = torch.randn(N, C, H, W, device=DEV)
+    w = torch.randn(K, C, R, R, device=DEV) * 0.1
+    b = torch.randn(K, device=DEV)
+    ref = _lib.qconv2d(x, w, b, st, pad, 1, 1, 4, "none")
+    sc = _lib.SplitConv(x.shape, w, st, pad, 1, 1, 4, "none")
+    sc.pack()
+    y = sc.conv(x, b)
+    assert ((y - ref).abs().max() / ref.abs().max()).item() <= CONV_TOL

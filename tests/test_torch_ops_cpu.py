@@ -43,3 +43,35 @@ def test_s2ds_meta_shapes_match_both_convs(C, H, W):
     y, yds = _lib.ops().qconv2d_s2ds(x, w, wds, 4, 1)
     assert y.shape == torch.nn.functional.conv2d(x, w, None, 2, 1).shape
     assert yds.shape == torch.nn.functional.conv2d(x, wds, None, 2, 0).shape
+
+
+def test_chain_and_pack_ops_registered_with_meta_shapes():
+    """qconv2d_chain (a stage's stride-1 run in one launch), qconv2d_pack_batch (the batched weight
+    staging of a forward) and qconv2d_packed (a conv from that workspace) are torch.ops with Meta
+    kernels: the output shapes F.conv2d gives, one workspace per layer."""
+    O = _lib.ops()
+    x = torch.empty(4, 16, 32, 32, device="meta")
+    ws = [torch.empty(16, 16, 3, 3, device="meta") for _ in range(3)]
+    assert O.qconv2d_chain(x, ws, 4, 1, 1, [], [], [], [1, 1, 1], [-1, 0, -1]).shape == x.shape
+    assert "Tensor[] weights" in str(O.qconv2d_chain.default._schema)
+    # two layers: a stage-3 3x3 (a row kernel reading a packed weight) and a depthwise 3x3
+    w3 = torch.empty(64, 64, 3, 3, device="meta")
+    wd = torch.empty(96, 1, 3, 3, device="meta")
+    geom = [256, 64, 56, 56, 1, 1, 1, 1, 1, 1, 1] + [8, 96, 16, 16, 1, 1, 1, 1, 1, 1, 96]
+    out = O.qconv2d_pack_batch([w3, wd], geom, 4, 1, 1, 0, [-1, -1])
+    assert len(out) == 2 and all(t.dtype == torch.uint8 and t.dim() == 1 for t in out)
+    xs = torch.empty(256, 64, 56, 56, device="meta")
+    y = O.qconv2d_packed(xs, w3, out[0], None, [1, 1], [1, 1], [1, 1], 1, 4, 1, 1, 0, -1, None, None, None, 1)
+    assert y.shape == torch.nn.functional.conv2d(xs, w3, None, 1, 1).shape
+    with pytest.raises(RuntimeError, match="bad lists|11 geometry"):
+        O.qconv2d_pack_batch([w3], geom, 4, 1)
+
+
+def test_chain_list_lengths_checked():
+    """a per-layer list shorter or longer than the weights is an error (it was silently
+    zero-filled: act none, no epilogue, res_from 0 = 'add x')."""
+    x = torch.empty(2, 16, 8, 8)
+    w = [torch.empty(16, 16, 3, 3)] * 3
+    for kw in ({"acts": ["relu"] * 2}, {"res_from": [-1, 0]}, {"biases": [None] * 4}, {"post_scales": []}):
+        with pytest.raises(_lib.Po2qError, match="one entry per weight"):
+            _lib.qconv2d_chain(x, w, **kw)
