@@ -58,6 +58,17 @@ const char* po2q_last_error(void);
 size_t po2q_quantize_workspace_bytes(int64_t n);
 int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, int mode,
                       void* workspace, size_t workspace_bytes, void* stream);
+/*
+ * The same for fp64 and bf16 weights, in the weight's dtype as the reference computes it (its
+ * torch ops keep the input dtype): fp64 with double arithmetic; bf16 (w, out as bf16 bit
+ * patterns) with torch's bf16 arithmetic, every step in fp32 rounded to bf16.  Bit-exact with the
+ * reference run on CPU in that dtype (decision tables measured from it,
+ * tests/golden/gen_thresholds_dtypes.py).  Same workspace size function.
+ */
+int po2q_quantize_f64(const double* w, double* out, int64_t n, int bits, int fsr, int mode,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int po2q_quantize_bf16(const uint16_t* w, uint16_t* out, int64_t n, int bits, int fsr, int mode,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /*
  * Linear power-of-two quantizers lin / lin+ (per input channel = dim 1 of a 4-D weight).

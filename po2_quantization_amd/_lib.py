@@ -9,9 +9,9 @@ planning / tuning / diagnostic entry points, the two-enqueue SplitConv, and ever
 PO2Q_LIB points at another build of libpo2q.so (diagnostic builds).
 
 fp32 HIP tensors always run the native kernels: a missing library raises, there is no
-torch fallback for them.  Only the PO2 / PO2+ quantizer accepts other inputs (CPU tensors,
-fp64, bf16, ...): those take restated_quantize, the reference formula written as torch ops
-in the input's own dtype and device (the reference preserves dtype).
+torch fallback for them.  The PO2 / PO2+ quantizer also takes fp64 and bf16 HIP tensors natively
+(the reference preserves dtype); other inputs (CPU tensors, fp16, ...) take
+restated_quantize, the reference formula written as torch ops in the input's dtype and device.
 """
 import ctypes
 import os
@@ -34,6 +34,8 @@ EXPORTS = (
     "po2q_last_error",
     "po2q_quantize_workspace_bytes",
     "po2q_quantize_f32",
+    "po2q_quantize_f64",
+    "po2q_quantize_bf16",
     "po2q_quantize_lin_f32",
     "po2q_qconv2d_workspace_bytes",
     "po2q_qconv2d_f32",
@@ -199,15 +201,12 @@ def _workspace(nbytes, dev):
 
 
 def restated_quantize(w, bits, mode, fsr=1):
-    """PO2 / PO2+ for inputs the native kernel does not take (CPU tensors, fp64, bf16, ...):
-    the reference's elementwise formula (utils/quantizers.py:21-32, :41-52) as torch ops in
-    w's own dtype and device, so torch's log2 / round of that device decide.  On CPU tensors
-    that is the reference's own arithmetic: bit for bit its outputs in every dtype
-    (tests/test_restated_quantizer.py).  On HIP tensors the device's log2 can land on the other
-    side of a rounding tie than the CPU's near k + 1/2: up to 0.5 % of the elements one
-    exponent step off the reference's CPU result (tests/test_gpu_quantizer.py, what the
-    reference's formula itself does on a GPU).  Product code for those inputs only; fp32 HIP
-    tensors always take the native, bit-exact kernel."""
+    """PO2 / PO2+ for inputs the native kernels do not take (CPU tensors; fp16 and other dtypes on
+    the GPU): the reference's elementwise formula (utils/quantizers.py:21-32, :41-52) as torch ops in
+    w's own dtype and device, so torch's log2 / round of that device decide.  On CPU tensors that is
+    the reference's own arithmetic: bit for bit its outputs in every dtype
+    (tests/test_restated_quantizer.py).  fp32, fp64 and bf16 HIP tensors take the native kernels,
+    bit-exact with the reference's CPU results (tests/test_gpu_quantizer.py)."""
     scale = torch.max(torch.abs(w))  # (raises for an empty tensor, as the reference does)
     a = (w / scale).abs()
     t = torch.log2(a / 1.5) + 0.5 if mode == "po2+" else torch.log2(a)
@@ -217,7 +216,9 @@ def restated_quantize(w, bits, mode, fsr=1):
     # pow(2, e) need not be (it is not for fp64 on the GPU), the CPU reference's is
     levels = torch.tensor([2.0 ** k for k in range(lo, hi + 1)], dtype=w.dtype, device=w.device)
     nan = torch.isnan(e)
-    p2 = levels[torch.where(nan, lo, e).long() - lo]
+    # (a bf16 clamp bound below -256 is itself rounded, e.g. -2047 -> -2048: such e are far below
+    # bf16's range, 2**e == 0 either way, so the index is clamped into the table)
+    p2 = levels[(torch.where(nan, lo, e).long() - lo).clamp(0, hi - lo)]
     p2 = torch.where(nan, e, p2)
     return p2 * torch.sign(w) * scale
 
@@ -229,13 +230,16 @@ def quantize(w, bits, mode, fsr=1):
     mode_id = MODES[mode]
     if mode_id == 0:
         raise Po2qError("po2q: quantize() needs mode 'po2' or 'po2+'")
-    if w.device.type != "cuda" or w.dtype != torch.float32:
+    native = w.device.type == "cuda" and w.dtype in (torch.float32, torch.float64, torch.bfloat16)
+    if not native:
         return restated_quantize(w, int(bits), mode, int(fsr))
     if w.numel() == 0:
         raise Po2qError("po2q: max(): Expected reduction dim to be specified for input.numel() == 0")
     O = ops()
     if O is not None:
         return _op_call(O.quantize, w, int(bits), mode_id, int(fsr))
+    if w.dtype != torch.float32:
+        raise Po2qError("po2q: fp64 / bf16 quantize needs the operator library (PO2Q_LIB selects another build)")
     L = load()
     wc = w.contiguous()
     out = torch.empty_like(wc)

@@ -54,7 +54,7 @@ const char* po2q_last_error(void) { return g_last_error.c_str(); }
 
 size_t po2q_quantize_workspace_bytes(int64_t n) {
     if (n <= 0) return 0;
-    return align_up((size_t)absmax_blocks(n) * sizeof(unsigned));
+    return align_up((size_t)absmax_blocks(n) * sizeof(uint64_t));  // fp64 partials are 8 bytes
 }
 
 int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, int mode, void* workspace,
@@ -78,6 +78,42 @@ int po2q_quantize_f32(const float* w, float* out, int64_t n, int bits, int fsr, 
     int st = hip_status(launch_absmax(w, n, partial, nb, s), "absmax launch");
     if (st) return st;
     return hip_status(launch_quantize_plain(w, n, partial, nb, bits, fsr, mode, out, s), "quantize launch");
+}
+
+}  // extern "C"
+
+// fp64 / bf16 weights (the reference keeps the dtype, quantizers.py:19-56)
+template <typename T>
+static int quantize_dt(const T* w, T* out, int64_t n, int bits, int fsr, int mode, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+    if (n <= 0) {
+        set_error("po2q: max(): Expected reduction dim to be specified for input.numel() == 0");
+        return PO2Q_ERR_INVALID;
+    }
+    if (!check_mode_bits(mode, bits, false)) return PO2Q_ERR_INVALID;
+    if (!w || !out || !workspace) {
+        set_error("po2q: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    if (workspace_bytes < po2q_quantize_workspace_bytes(n)) {
+        set_error("po2q: quantize workspace too small");
+        return PO2Q_ERR_WORKSPACE;
+    }
+    return hip_status(launch_quantize_dt<T>(w, out, n, bits, fsr, mode, reinterpret_cast<uint64_t*>(workspace),
+                                            absmax_blocks(n), reinterpret_cast<hipStream_t>(stream)),
+                      "quantize launch");
+}
+
+extern "C" {
+
+int po2q_quantize_f64(const double* w, double* out, int64_t n, int bits, int fsr, int mode, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+    return quantize_dt<double>(w, out, n, bits, fsr, mode, workspace, workspace_bytes, stream);
+}
+
+int po2q_quantize_bf16(const uint16_t* w, uint16_t* out, int64_t n, int bits, int fsr, int mode, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+    return quantize_dt<uint16_t>(w, out, n, bits, fsr, mode, workspace, workspace_bytes, stream);
 }
 
 int po2q_quantize_lin_f32(const float* w, float* out, int64_t d0, int64_t d1, int64_t d2, int64_t d3, int bits,

@@ -191,6 +191,12 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
 hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
                                   const float* scale, const float* bias, float* y, hipStream_t s);
 
+// fp64 / bf16 (bit patterns) PO2 / PO2+ quantizer (po2q_quant_dtypes.hip): absmax partials
+// (nparts = absmax_blocks(n) uint64 words), then the quantize pass.
+template <typename T>
+hipError_t launch_quantize_dt(const T* w, T* out, int64_t n, int bits, int fsr, int mode, uint64_t* partial,
+                              int nparts, hipStream_t s);
+
 // lin / lin+ quantizer (po2q_lin.hip): w, out [d0, d1, rs = d2*d3], one block per d1 channel
 hipError_t launch_quantize_lin(const float* w, float* out, int d0, int d1, int rs, int bits, int num_iters, int plus,
                                hipStream_t s);

@@ -4,7 +4,7 @@
 // resolved plan handle + workspace size per conv problem, and launches on torch's current
 // HIP stream.  Replaces the reference's call sites:
 //   po2q::quantize       PowerOfTwoQuantizer / PowerOfTwoPlusQuantizer.forward
-//                        (utils/quantizers.py:19-56)
+//                        (utils/quantizers.py:19-56), fp32 / fp64 / bf16 (the reference keeps the dtype)
 //   po2q::quantize_lin   LinearPowerOfTwo(Plus)Quantizer.forward (utils/quantizers.py:59-136)
 //   po2q::qconv2d        QuantizedConv2d.forward: F.conv2d(x, Q(w), bias, ...)
 //                        (models/quantized_conv.py:32-38)
@@ -232,7 +232,11 @@ at::Tensor qconv2d_fused(const at::Tensor& x, const at::Tensor& w, const c10::op
 }
 
 at::Tensor quantize(const at::Tensor& w_, int64_t bits, int64_t mode, int64_t fsr) {
-    check_hip_f32(w_, "input");
+    TORCH_CHECK(w_.is_cuda(), "po2q: input must be a HIP device tensor (got ", w_.device(),
+                "); the po2q ops have no CPU path");
+    const auto dt = w_.scalar_type();
+    TORCH_CHECK(dt == at::kFloat || dt == at::kDouble || dt == at::kBFloat16,
+                "po2q: quantize takes float32, float64 or bfloat16 (got ", dt, ")");
     TORCH_CHECK(mode == 1 || mode == 2, "po2q: quantize() needs mode po2 (1) or po2+ (2)");
     const DeviceGuard guard(w_.device());
     const at::Tensor w = w_.contiguous();
@@ -240,8 +244,16 @@ at::Tensor quantize(const at::Tensor& w_, int64_t bits, int64_t mode, int64_t fs
     const int64_t n = w.numel();
     at::Tensor ws = at::empty({(int64_t)std::max<size_t>(po2q_quantize_workspace_bytes(n), 256)},
                               w.options().dtype(at::kByte));
-    const int st = po2q_quantize_f32(w.data_ptr<float>(), out.data_ptr<float>(), n, (int)bits, (int)fsr, (int)mode,
-                                     ws.data_ptr(), ws.numel(), stream_of(w));
+    int st;
+    if (dt == at::kFloat)
+        st = po2q_quantize_f32(w.data_ptr<float>(), out.data_ptr<float>(), n, (int)bits, (int)fsr, (int)mode,
+                               ws.data_ptr(), ws.numel(), stream_of(w));
+    else if (dt == at::kDouble)
+        st = po2q_quantize_f64(w.data_ptr<double>(), out.data_ptr<double>(), n, (int)bits, (int)fsr, (int)mode,
+                               ws.data_ptr(), ws.numel(), stream_of(w));
+    else
+        st = po2q_quantize_bf16(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                n, (int)bits, (int)fsr, (int)mode, ws.data_ptr(), ws.numel(), stream_of(w));
     TORCH_CHECK(st == 0, last_error());
     return out;
 }

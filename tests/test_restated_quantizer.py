@@ -47,3 +47,23 @@ def test_restatement_bit_exact_on_fp64_bf16_golden_vectors():
             torch.equal(torch.isnan(y), torch.isnan(want)) and torch.equal(y[~torch.isnan(y)], want[~torch.isnan(want)]), key
         n += 1
     assert n == 48
+
+
+def test_restatement_bit_exact_on_extended_dtype_vectors():
+    """The extended fp64 / bf16 vectors (quant_kat_dtypes2.npz, the GPU kernels' pins) through the
+    CPU restatement: checks the fixture against an independent route to the reference's numbers."""
+    d = load_npz("quant_kat_dtypes2.npz")
+    n = 0
+    for key in d.files:
+        if not key.startswith("y/"):
+            continue
+        _, dt, name, mode, bits, fsr = key.split("/")
+        x = _load(d["x/%s/%s" % (dt, name)], dt)
+        y = _lib.restated_quantize(x, int(bits), mode, int(fsr))
+        want = _load(d[key], dt)
+        iv = torch.int16 if dt == "bf16" else torch.int64
+        nan = torch.isnan(y)
+        assert torch.equal(nan, torch.isnan(want)), key
+        assert torch.equal(y.view(iv)[~nan], want.view(iv)[~nan]), key
+        n += 1
+    assert n == 192
