@@ -27,6 +27,11 @@
 #include <cstdint>
 #include <string>
 #include <type_traits>
+#ifdef PO2Q_PAIR_STAMPS
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#endif
 
 #include "../../include/po2q.h"
 #include "po2q_epi.h"
@@ -61,7 +66,27 @@ struct PairArgs {
     int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
     int halves;        // unused (the half-line A/B knob of round 2: C = 16 always stores whole lines)
     int stg;           // 1: the stagger (STG) kernel for the forms without a residual
+    unsigned* stamps;  // PO2Q_PAIR_STAMPS diagnostic builds only: per-wave phase cycle sums
 };
+
+// Diagnostic build (-DPO2Q_PAIR_STAMPS, `make pairstamps`): s_memtime phase stamps (guide "In-kernel
+// stamps"; the sched_barriers serialize each phase, so read the shares, not the total); never in
+// the product build.
+#ifdef PO2Q_PAIR_STAMPS
+#define PO2Q_PSTAMP(i)                                                                   \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        ph_[i] += (unsigned)(t_ - tprev_);                                               \
+        tprev_ = t_;                                                                     \
+    } while (0)
+#else
+#define PO2Q_PSTAMP(i) \
+    do {               \
+    } while (0)
+#endif
 
 // Byte offset of the 16-byte channel octet `oc` (channels 8 oc .. 8 oc + 7) of pixel P in a
 // shared intermediate plane ([pixel][C] bf16, 2C bytes per pixel), XOR-swizzled at octet
@@ -411,6 +436,10 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     const bool strip_full = q0 + SW <= a.W;  // wave-uniform
     // the stagger's late waves (wave-uniform: an SGPR branch)
     const bool late = STG != 0 && wave >= 4;
+#ifdef PO2Q_PAIR_STAMPS
+    unsigned ph_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev_ = 0;
+#endif
 
     auto step = [&](auto S_, int j) __attribute__((always_inline)) {
         constexpr int S6 = decltype(S_)::value;
@@ -419,8 +448,11 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         constexpr int YW = S6 & 1;              // ring slot written: intermediate row j-2
         constexpr int YR = (S6 + 1) & 1;        // ring slot read: intermediate row j-3
         const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
+        PO2Q_PSTAMP(0);
         rows_wait<VMW>();  // this wave's part of x row j has landed
+        PO2Q_PSTAMP(1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + everyone's plane writes
+        PO2Q_PSTAMP(2);
         load_row((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
         // the x split's LDS reads next: their latency runs under conv 2's MFMAs
         uint32_t bx[8], hx;
@@ -442,13 +474,17 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         // no branch, so its MFMAs interleave with the epilogue-2 and x-split vector work below)
         if constexpr ((DBG & 1) == 0)
             mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
+        PO2Q_PSTAMP(3);
         if (!late) {
             epi2(S_, j);
+            PO2Q_PSTAMP(4);
             split_x(bx, hx);
+            PO2Q_PSTAMP(5);
         }
 
         // ---- conv 1 on x row j (transposed MFMAs); intermediate row i = j - 2 completes
         if constexpr ((DBG & 2) == 0) mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, bw2, slab);
+        PO2Q_PSTAMP(6);
         if constexpr ((DBG & 16) == 0) {
             const int i = j - 2;
             const int r1 = p0 - 1 + i;
@@ -497,6 +533,10 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
                 }
             }
         }
+        PO2Q_PSTAMP(7);
+#ifdef PO2Q_PAIR_STAMPS
+        ph_[8] += 1;
+#endif
     };
 
     {
@@ -581,6 +621,9 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     }
     // static priority for the younger wave of each SIMD (MI355X_MICROARCH two-waves item 4)
     if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+#ifdef PO2Q_PAIR_STAMPS
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
+#endif
     int jl = 0;  // the last step run (its S6 is 2 or 5: both complete accumulator slot 1)
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
@@ -597,6 +640,10 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         if (late) epi2(std::integral_constant<int, 2>{}, jl);  // the deferred last epilogue
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
+#ifdef PO2Q_PAIR_STAMPS
+    if (lane == 0 && a.stamps)
+        for (int i = 0; i < 9; ++i) a.stamps[((size_t)blockIdx.x * 8 + wave) * 9 + i] = ph_[i];
+#endif
 }
 
 
@@ -972,6 +1019,32 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
     const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
     const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
     constexpr bool kStg = PD == 2 && NTS == 3;  // the stagger is instantiated for the default ring / store mode
+#ifdef PO2Q_PAIR_STAMPS
+    if (plain && getenv("PO2Q_STAMPS")) {
+        PairArgs as = a;
+        const size_t nst = (size_t)pp.blocks * 8 * 9;
+        if (hipMalloc(&as.stamps, nst * 4) == hipSuccess) {
+            (void)hipMemsetAsync(as.stamps, 0, nst * 4, s);
+            hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, as);
+            std::vector<unsigned> h(nst);
+            (void)hipStreamSynchronize(s);
+            (void)hipMemcpy(h.data(), as.stamps, nst * 4, hipMemcpyDeviceToHost);
+            (void)hipFree(as.stamps);
+            double sum[9] = {0};
+            for (size_t i = 0; i < nst; ++i) sum[i % 9] += h[i];
+            const double waves = (double)pp.blocks * pp.waves, steps = sum[8] / waves;
+            static const char* names[8] = {"top->wait", "vmcnt-wait", "barrier", "conv2-mfma", "epi2",
+                                           "split-x", "conv1-mfma", "epi1"};
+            double tot = 0;
+            for (int i = 0; i < 8; ++i) tot += sum[i];
+            fprintf(stderr, "[po2q stamps] C=%d blocks=%lld waves/block=%d steps/wave=%.1f cycles/step/wave=%.0f\n", CC,
+                    (long long)pp.blocks, pp.waves, steps, tot / waves / steps);
+            for (int i = 0; i < 8; ++i)
+                fprintf(stderr, "  %-11s %8.0f cyc/step  %5.1f%%\n", names[i], sum[i] / waves / steps, 100.0 * sum[i] / tot);
+            return hipGetLastError();
+        }
+    }
+#endif
     if (kStg && plain && a.stg)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
     else if (plain)
@@ -1152,6 +1225,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.prio = prio;
     a.halves = halves;
     a.stg = stg;
+    a.stamps = nullptr;
     if (stg == 2 && C == 16 && !residual && W <= 4 * po2q::kABSW) {
         // role-split kernel: 2 x ceil(W / 64) waves, the pair plan's row segments
         po2q::PairABArgs b;

@@ -192,7 +192,7 @@ def batched_packs(model, x):
             or not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32)):
         yield
         return
-    key = (tuple(x.shape), x.device)
+    key = (tuple(x.shape), x.device, INFERENCE_FUSION)
     rec = model.__dict__.setdefault("_po2q_packs", {})
     sess = _ForwardPacks(rec.get(key))
     _packs = sess

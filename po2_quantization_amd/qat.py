@@ -11,6 +11,9 @@ reference's train.py loop, one process per GPU, DistributedDataParallel over RCC
   train_step(...)                 train.py:79-94   forward (fused native quantize + conv), CE
                                                    loss, backward (STE + conv grads; DDP
                                                    all-reduces the gradient buckets), SGD step
+  GraphedTrainStep                train.py:79-94   the same step captured once in a HIP graph and
+                                                   replayed (single process): ~1000 host launches
+                                                   per step become one graph launch
   run_train_loop(...)             train.py:37-125  epochs, per-epoch all_reduce of loss/samples,
                                                    quantization error, rows for the CSV
   write_train_csv(path, rows)     train.py:255-259 header epoch,train_loss,train_acc,quantization_error
@@ -110,6 +113,81 @@ def train_step(model: nn.Module, optimizer, criterion, images: torch.Tensor, lab
     return loss.detach() * images.size(0), correct
 
 
+class GraphedTrainStep:
+    """train_step (train.py:79-94) captured in a HIP graph and replayed: forward (the fused native
+    quantize + conv kernels), cross-entropy, the native backward and the SGD update as one graph
+    launch.  At CIFAR size the eager step is bound by ~1000 host-side launches (BatchNorm, autograd,
+    the optimizer), not by the convs; the replay issues none of them from the host.
+
+    Same arithmetic as the eager step (the same kernels on the same tensors).  The batch is copied
+    into static input buffers; step() returns (loss * batch, correct) as device tensors like
+    train_step.  The learning rate is a Python float inside the SGD update, so the step is
+    re-captured when a scheduler changes it (once per epoch).  Single process only (DDP's bucketed
+    all-reduce is not captured here); the po2q autotuner runs in the eager warm-up steps, before
+    capture (it synchronises the stream)."""
+
+    def __init__(self, model: nn.Module, optimizer, criterion, images: torch.Tensor, labels: torch.Tensor,
+                 warmup: int = 3):
+        _, world = _world()
+        if world > 1 or isinstance(model, DistributedDataParallel):
+            raise RuntimeError("GraphedTrainStep: single-process training only")
+        self.model, self.optimizer, self.criterion = model, optimizer, criterion
+        self.x = images.clone()
+        self.y = labels.clone()
+        self.warmup = warmup
+        self.graph = None
+        self._lr = None
+
+    def _lrs(self):
+        return tuple(float(g["lr"]) for g in self.optimizer.param_groups)
+
+    def _state(self):
+        """Every tensor a step mutates: parameters, buffers (BatchNorm statistics and counters) and the
+        optimizer's momentum buffers."""
+        ts = list(self.model.state_dict(keep_vars=True).values())
+        for group in self.optimizer.param_groups:
+            for p in group["params"]:
+                buf = self.optimizer.state.get(p, {}).get("momentum_buffer")
+                if buf is not None:
+                    ts.append(buf)
+        return [t.detach() if isinstance(t, torch.Tensor) else t for t in ts]
+
+    def _capture(self):
+        if self.graph is None:
+            # eager warm-up on a side stream (po2q autotuning, lazy allocations, the optimizer's
+            # momentum buffers), then every mutated tensor restored: the warm-up leaves no trace
+            before = {id(t): t.clone() for t in self._state()}
+            s = torch.cuda.Stream(self.x.device)
+            s.wait_stream(torch.cuda.current_stream(self.x.device))
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    train_step(self.model, self.optimizer, self.criterion, self.x, self.y)
+            torch.cuda.current_stream(self.x.device).wait_stream(s)
+            with torch.no_grad():
+                for t in self._state():
+                    if id(t) in before:
+                        t.copy_(before[id(t)])
+                    else:  # a momentum buffer the warm-up created: zero gives SGD's first-step update
+                        t.zero_()
+        self.optimizer.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):  # records only: nothing runs until replay
+            self.out = train_step(self.model, self.optimizer, self.criterion, self.x, self.y)
+        self.graph = g
+        self._lr = self._lrs()
+
+    def step(self, images: torch.Tensor, labels: torch.Tensor):
+        if tuple(images.shape) != tuple(self.x.shape) or tuple(labels.shape) != tuple(self.y.shape):
+            raise RuntimeError("GraphedTrainStep: the batch shape changed (%s); capture another step"
+                               % (tuple(images.shape),))
+        self.x.copy_(images, non_blocking=True)
+        self.y.copy_(labels, non_blocking=True)
+        if self.graph is None or self._lrs() != self._lr:
+            self._capture()
+        self.graph.replay()
+        return self.out[0].clone(), self.out[1].clone()
+
+
 def shard_batches(images: torch.Tensor, labels: torch.Tensor, batch_size: int, epoch: int, seed: int = 0):
     """DistributedSampler(shuffle=True) order for this rank, in batches."""
     rank, world = _world()
@@ -121,8 +199,11 @@ def shard_batches(images: torch.Tensor, labels: torch.Tensor, batch_size: int, e
 
 
 def run_train_loop(model: nn.Module, device, images: torch.Tensor, labels: torch.Tensor, batch_size: int,
-                   model_path: Optional[str], num_epochs: int, lr: float, log=print) -> List[Row]:
-    """train.py:37-125; returns (epoch, train_loss, train_acc, quantization_error) rows."""
+                   model_path: Optional[str], num_epochs: int, lr: float, log=print,
+                   graph: bool = False) -> List[Row]:
+    """train.py:37-125; returns (epoch, train_loss, train_acc, quantization_error) rows.
+    graph=True (single process, HIP device): full batches run as a GraphedTrainStep replay, a
+    trailing partial batch eagerly."""
     rank, world = _world()
     optimizer, warmup, multistep, warmup_epochs = make_optimizer(model, lr, num_epochs)
     criterion = nn.CrossEntropyLoss()
@@ -130,6 +211,7 @@ def run_train_loop(model: nn.Module, device, images: torch.Tensor, labels: torch
     if world > 1:
         dist.barrier()
     core = model.module if isinstance(model, DistributedDataParallel) else model
+    graphed = None
     for epoch in range(num_epochs):
         total_loss = torch.zeros((), dtype=torch.float32, device=device)
         total_samples = torch.zeros((), dtype=torch.int64, device=device)
@@ -137,7 +219,12 @@ def run_train_loop(model: nn.Module, device, images: torch.Tensor, labels: torch
         model.train()
         for x, y in shard_batches(images, labels, batch_size, epoch):
             x, y = x.to(device), y.to(device)
-            ls, c = train_step(model, optimizer, criterion, x, y)
+            if graph and world == 1 and x.is_cuda and x.size(0) == batch_size:
+                if graphed is None:
+                    graphed = GraphedTrainStep(model, optimizer, criterion, x, y)
+                ls, c = graphed.step(x, y)
+            else:
+                ls, c = train_step(model, optimizer, criterion, x, y)
             total_loss += ls
             total_correct += c
             total_samples += y.size(0)

@@ -94,3 +94,42 @@ def test_ddp_two_ranks_stay_in_lockstep(tmp_path):
     p = torch.load(out, weights_only=True)
     assert torch.equal(p[0], p[1])  # averaged gradients -> identical updates
     assert _lib.load() is not None
+
+
+def test_graphed_train_step_equals_eager_steps():
+    """GraphedTrainStep (the whole QAT step -- fused native forward, native backward, SGD -- replayed
+    from one HIP graph) against the same steps run eagerly from the same initial
+    state: the warm-up leaves no trace and every replay is the eager step's arithmetic."""
+    torch.backends.cudnn.benchmark = False
+    g = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(16, 3, 32, 32, generator=g).to(DEV), torch.randint(0, 10, (16,), generator=g).to(DEV))
+               for _ in range(4)]
+
+    def make():
+        torch.manual_seed(3)
+        m = qat.build_model("resnet20", 10, quantizer_dict["po2"], 4, (32, 32), torch.device(DEV))
+        opt, _, _, _ = qat.make_optimizer(m, 0.05, 10)
+        return m, opt
+
+    crit = torch.nn.CrossEntropyLoss()
+    m1, o1 = make()
+    for x, y in batches:
+        l1, c1 = qat.train_step(m1, o1, crit, x, y)
+    m2, o2 = make()
+    gs = qat.GraphedTrainStep(m2, o2, crit, batches[0][0], batches[0][1])
+    for x, y in batches:
+        l2, c2 = gs.step(x, y)
+    torch.cuda.synchronize()
+    assert gs.graph is not None
+    for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
+        if a.is_floating_point():
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), k
+        else:
+            assert torch.equal(a, b), k
+    assert torch.allclose(l1, l2, rtol=1e-4) and torch.equal(c1, c2)
+    # a learning-rate change re-captures the step
+    for grp in o2.param_groups:
+        grp["lr"] *= 0.1
+    first = gs.graph
+    gs.step(*batches[0])
+    assert gs.graph is not first

@@ -1,5 +1,6 @@
 """QAT training-step throughput (config 2: ResNet56, CIFAR 32x32,
-bs=256, po2 4-bit): forward (fused native quantize + conv) + STE backward + SGD step,
+bs=256, po2 4-bit): forward (fused native quantize + conv) + STE backward + SGD step, eager and
+replayed from one HIP graph (qat.GraphedTrainStep),
 against the same step with the reference's torch-op QuantizedConv2d.forward
 (quantize in torch ops via the native quantizer + F.conv2d; quantized_conv.py:32-38).
 GPU only; one JSON line per configuration.  Synthetic data."""
@@ -23,7 +24,7 @@ def torch_forward(self, input):
     return F.conv2d(input, w, self.bias, self.stride, self.padding, self.dilation, self.groups)
 
 
-def run(model_type, qn, bits, bs, steps=20, warmup=5):
+def run(model_type, qn, bits, bs, steps=20, warmup=5, graph=False):
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
     m = qat.build_model(model_type, 10, quantizer_dict[qn], bits, (32, 32), dev)
@@ -31,13 +32,18 @@ def run(model_type, qn, bits, bs, steps=20, warmup=5):
     crit = torch.nn.CrossEntropyLoss()
     x = torch.randn(bs, 3, 32, 32, device=dev)
     y = torch.randint(0, 10, (bs,), device=dev)
+    if graph:  # the whole step replayed from one HIP graph (qat.GraphedTrainStep)
+        gs = qat.GraphedTrainStep(m, opt, crit, x, y)
+        step = lambda: gs.step(x, y)  # noqa: E731
+    else:
+        step = lambda: qat.train_step(m, opt, crit, x, y)  # noqa: E731
     for _ in range(warmup):
-        qat.train_step(m, opt, crit, x, y)
+        step()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(steps):
-        qat.train_step(m, opt, crit, x, y)
+        step()
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / steps
@@ -54,6 +60,7 @@ def main():
         if only and model_type not in only:
             continue
         ms, ips = run(model_type, qn, bits, 256)
+        ms_g, ips_g = run(model_type, qn, bits, 256, graph=True)
         QC.NATIVE_BACKWARD = False
         try:
             ms_a, ips_a = run(model_type, qn, bits, 256)
@@ -67,6 +74,7 @@ def main():
             QC.QuantizedConv2d.forward = orig
         print(json.dumps({"model": model_type, "quantizer": qn, "bits": bits, "batch": 256, "image": 32,
                           "native_ms_per_step": round(ms, 3), "native_images_per_s": round(ips, 1),
+                          "graph_ms_per_step": round(ms_g, 3), "graph_images_per_s": round(ips_g, 1),
                           "aten_backward_ms_per_step": round(ms_a, 3), "aten_backward_images_per_s": round(ips_a, 1),
                           "miopen_find": torch.backends.cudnn.benchmark,
                           "torch_forward_ms_per_step": round(ms_t, 3),
