@@ -440,9 +440,17 @@ def model_extra(args, world, rank, dev, model_type, quantizer, bits, image, batc
         with torch.cuda.stream(s):
             m_dev(x)
         torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
+        try:
+            graph = torch.cuda.CUDAGraph(keep_graph=True)  # keeps the raw graph for graph_launches
+        except TypeError:
+            graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             logits = m_dev(x)
+        if getattr(graph, "instantiate", None) is not None:
+            try:
+                graph.instantiate()
+            except Exception:  # noqa: BLE001 -- already instantiated
+                pass
         gathered = torch.empty(world * batch, classes, device=dev) if world > 1 else None
         gstep = lambda record=False: gather_logits(graph.replay() or logits, gathered, world)  # noqa: E731
         dt = timed_steps(gstep, steps, 5, world, torch.cuda.synchronize, dev)
@@ -478,23 +486,65 @@ def model_extra(args, world, rank, dev, model_type, quantizer, bits, image, batc
     flops = 2.0 * N * K * P * Q * Cg * R * S
     achieved = nbytes / (ms * 1e-3) / 1e9
     plan = _lib.describe(N, C, H, W, K, R, S, st, pad, dil, grp, bits, mode)
+    # step level: the algorithmic bytes of every conv call of the forward (fp32 x in + y out + the
+    # weight read once; BN / activation / residual are fused into those) over the measured step
+    step_bytes, step_flops = 0.0, 0.0
+    for (xs_, ws_, st_, pad_, dil_, grp_, _), (cnt_, _) in calls.items():
+        n_, c_, h_, w_ = xs_
+        k_, cg_, r_, s_ = ws_
+        p_ = (h_ + 2 * pad_[0] - dil_[0] * (r_ - 1) - 1) // st_[0] + 1
+        q_ = (w_ + 2 * pad_[1] - dil_[1] * (s_ - 1) - 1) // st_[1] + 1
+        step_bytes += cnt_ * 4.0 * (n_ * c_ * h_ * w_ + n_ * k_ * p_ * q_ + k_ * cg_ * r_ * s_)
+        step_flops += cnt_ * 2.0 * n_ * k_ * p_ * q_ * cg_ * r_ * s_
+    step_ms = dt * 1e3 / steps
+    step_achieved = step_bytes / (step_ms * 1e-3) / 1e9
     images = world * batch * steps
     out = {"workload": "%s @%dx%d bs=%d per GPU, %s %d-bit QAT-mode weights, fused eval forward (every conv + BN + "
                        "act + residual native), HIP graph replay" % (model_type, image, image, batch, quantizer, bits),
            "metric": "%s fwd images/sec, %s %dx%d bs=%d" % (label, model_type, image, image, batch),
            "value": round(images / dt, 2), "unit": "images/s", "n_gpus": world, "steps": steps,
-           "ms_per_step": round(dt * 1e3 / steps, 4),
-           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                        "kernel": "fused %s quantize+conv %dx%d s%d g%d %d->%d @%dx%d bs=%d (%d calls per forward): %s"
-                                  % (mode, R, S, st[0], grp, C, K, H, W, N, cnt, plan),
-                        "avg_launch_ms": round(ms, 5), "algorithmic_bytes": int(nbytes), "flops": int(flops),
-                        "note": "latency-bound at this size: a layer's tensors are a few MB (Infinity-Cache "
-                                "resident between launches), so the HBM fraction is low by construction"},
+           "ms_per_step": round(step_ms, 4),
+           "roofline": {"scope": "step", "bound": "hbm", "achieved": round(step_achieved, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(step_achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": int(step_bytes), "flops_per_step": int(step_flops),
+                        "conv_calls_per_step": int(sum(c for c, _ in calls.values())),
+                        "launches_per_step": graph_launches(graph),
+                        "note": "the whole forward: every conv call's algorithmic bytes (x in + y out + weight) "
+                                "over ms_per_step; at this size the step is bound by launch latency (a few us of "
+                                "work per kernel), not by HBM or the matrix cores",
+                        "dominant_kernel": {
+                            "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": round(achieved / PEAK_HBM_GBS, 4),
+                            "kernel": "fused %s quantize+conv %dx%d s%d g%d %d->%d @%dx%d bs=%d (%d calls per "
+                                      "forward): %s" % (mode, R, S, st[0], grp, C, K, H, W, N, cnt, plan),
+                            "avg_launch_ms": round(ms, 5), "algorithmic_bytes": int(nbytes), "flops": int(flops)}},
            "cpu_baseline": None}
     if cpu:
         out["cpu_baseline"] = model_cpu_baseline(m, image, min(args.cpu_seconds, 10.0), label)
     return out
+
+
+def graph_launches(graph):
+    """Kernel nodes of a captured HIP graph (hipGraphGetNodes on torch's raw graph handle), or None
+    where this torch build does not expose the handle."""
+    try:
+        import ctypes
+        h = graph.raw_cuda_graph()
+        hip = ctypes.CDLL("libamdhip64.so")
+        n = ctypes.c_size_t(0)
+        if hip.hipGraphGetNodes(ctypes.c_void_p(h), None, ctypes.byref(n)) != 0:
+            return None
+        nodes = (ctypes.c_void_p * n.value)()
+        if hip.hipGraphGetNodes(ctypes.c_void_p(h), nodes, ctypes.byref(n)) != 0:
+            return None
+        kinds = ctypes.c_int(0)
+        kernels = 0
+        for nd in nodes:
+            if hip.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(kinds)) == 0 and kinds.value == 0:
+                kernels += 1  # hipGraphNodeTypeKernel
+        return kernels
+    except Exception:  # noqa: BLE001 -- diagnostic only
+        return None
 
 
 def model_cpu_baseline(m, image, seconds, label):

@@ -67,6 +67,7 @@ struct PairArgs {
     int halves;        // unused (the half-line A/B knob of round 2: C = 16 always stores whole lines)
     int stg;           // 1: the stagger (STG) kernel for the forms without a residual
     unsigned* stamps;  // PO2Q_PAIR_STAMPS diagnostic builds only: per-wave phase cycle sums
+    int mw;            // 1: the memory-wave kernel (MW) where it applies
 };
 
 // Diagnostic build (-DPO2Q_PAIR_STAMPS, `make pairstamps`): s_memtime phase stamps (guide "In-kernel
@@ -133,10 +134,16 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // DBG (diagnostic builds only, -DPO2Q_PAIR_DIAG, PO2Q_PAIR_DEBUG; timing only, outputs are
 // wrong): bit 1 no conv-2 MFMAs, 2 no conv-1 MFMAs, 4 no x DMAs, 8 no output stores, 16 no
 // split / epilogue-1 plane writes.
-template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0>
-__global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
+// MW 1 (memory wave): an eighth wave issues every x DMA of the block, PD - 1 rows ahead, and joins
+// the per-step barrier; the seven compute waves issue no loads, so they never wait on a vmcnt (their
+// stores are never waited for until the end).  Without it each compute wave waits, every step, for
+// its own x DMA of the previous step AND every store issued before it.  Plain / general forms
+// without a residual, seven compute waves (192 < W <= 224).
+template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0, int MW = 0>
+__global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
     static_assert(!(STG && RES), "stagger: the residual row's LDS slot is refilled before a deferred epilogue");
+    static_assert(!MW || (!RES && !STG && CC == 16), "memory wave: C = 16 forms without a residual or stagger");
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
     constexpr int SW = kQSW<CC>, WC = SW + 2, PL = kQPlane<CC>, KS = kQKS<CC>;
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nw = (int)(blockDim.x >> 6);
+    const int nw = (int)(blockDim.x >> 6) - MW;  // compute waves (MW: wave nw is the memory wave)
     const int rawslot = CC * a.Wp * 4;
     // the intermediate planes are sized for the widest image (7 waves): a compile-time pitch turns
     // every slot / plane offset of the fragment reads and epilogue writes into an immediate
@@ -449,11 +456,11 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
         constexpr int YR = (S6 + 1) & 1;        // ring slot read: intermediate row j-3
         const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
         PO2Q_PSTAMP(0);
-        rows_wait<VMW>();  // this wave's part of x row j has landed
+        if constexpr (!MW) rows_wait<VMW>();  // this wave's part of x row j has landed
         PO2Q_PSTAMP(1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + everyone's plane writes
         PO2Q_PSTAMP(2);
-        load_row((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
+        if constexpr (!MW) load_row((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
         // the x split's LDS reads next: their latency runs under conv 2's MFMAs
         uint32_t bx[8], hx;
         {
@@ -539,7 +546,27 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #endif
     };
 
-    {
+    // MW: the memory wave's DMA of x row jn into its raw ring slot: every float4 of the row's C x Wp/4
+    // (instruction i, lane l -> float4 64 i + l; the compute waves' own load_row split it 2 per wave)
+    auto mw_row = [&](int jn) __attribute__((always_inline)) {
+        const int h = p0 - 2 + jn;
+        const bool hok = jn < nx && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t base = raw_lds + (uint32_t)((jn % PD) * rawslot);
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const int e = 64 * i + lane;
+            const int c = e / W4, q = 4 * (e - c * W4);
+            const uint32_t vo = (hok && q < a.W) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u + roff : 0x7fffffffu;
+            rows_dma16<(NTS & 2) != 0>(rs, vo, 0u, base + (uint32_t)i * 1024u);
+        }
+    };
+    if constexpr (MW) {
+        if (wave == nw) {
+#pragma unroll
+            for (int r = 0; r < PD - 1; ++r) mw_row(r);
+        }
+    } else {
         // x rows 0 .. PD-2, each followed by ST dropped stores (the steady-state count)
         const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -554,13 +581,13 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
     {
         unsigned* red = reinterpret_cast<unsigned*>(yr);
         unsigned* thr = red + 16;
-        scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
+        scale1 = wq_prologue(a.q1, thr, red, nw + MW, fin1);
 #pragma unroll
         for (int f = 0; f < NF; ++f)
             bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr,
                                                              CC == 16));
         __syncthreads();  // red / thr reads of conv 1 done
-        scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
+        scale2 = wq_prologue(a.q2, thr, red, nw + MW, fin2);
         if constexpr (WL2) {
             for (int e = tid; e < NF * 64; e += blockDim.x) wl2[e] = wq_frag_rows(a.q2, CC, CC, CC, NT, KS, e, scale2, fin2, thr);
         } else {
@@ -624,6 +651,30 @@ __global__ __launch_bounds__(448, 1) void conv_pair(const float* __restrict__ x,
 #ifdef PO2Q_PAIR_STAMPS
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
 #endif
+    if constexpr (MW) {
+        if (wave == nw) {
+            // the memory wave: before barrier j row j has landed (its DMA is the oldest of the PD - 1
+            // rows in flight), after it the slot of row j - 1 (read by the splits of step j - 1, which
+            // every wave finished before the barrier) takes row j + PD - 1.  Same barrier count as the
+            // compute waves' loop.
+            auto mstep = [&](int j) __attribute__((always_inline)) {
+                rows_wait<14 * (PD - 2)>();
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                mw_row(j + PD - 1);
+            };
+            for (int j = 0; j < nsteps; j += 6) {
+                mstep(j);
+                mstep(j + 1);
+                mstep(j + 2);
+                if (j + 3 >= nsteps) break;
+                mstep(j + 3);
+                mstep(j + 4);
+                mstep(j + 5);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+    }
     int jl = 0;  // the last step run (its S6 is 2 or 5: both complete accumulator slot 1)
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
@@ -1045,6 +1096,16 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
         }
     }
 #endif
+    if constexpr (CC == 16 && PD >= 3 && (NTS == 3 || NTS == 1)) {
+        if (a.mw && pp.waves == 7 && !res) {  // the memory-wave kernel: 7 compute waves + 1
+            const dim3 block8(64 * 8);
+            if (plain)
+                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+            else
+                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+            return hipGetLastError();
+        }
+    }
     if (kStg && plain && a.stg)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
     else if (plain)
@@ -1081,7 +1142,7 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
     PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
     PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
     PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
-    PO2Q_PR(16, 3, 3) PO2Q_PR(16, 4, 3)
+    PO2Q_PR(16, 3, 3) PO2Q_PR(16, 4, 3) PO2Q_PR(16, 5, 3) PO2Q_PR(16, 6, 3)
 #undef PO2Q_PR
     return hipErrorInvalidValue;
 }
@@ -1115,7 +1176,7 @@ void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
         if (((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) ||
-            (C == 16 && (d == 3 || d == 4) && t == 3)) {
+            (C == 16 && d >= 3 && d <= 6 && t == 3)) {
             pd = d;
             nts = t;
         }
@@ -1226,6 +1287,20 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.halves = halves;
     a.stg = stg;
     a.stamps = nullptr;
+    // PO2Q_PAIR_MW = PD (3..6): the memory-wave kernel with a PD-slot x ring (A/B knob)
+    a.mw = 0;
+    if (const char* mv = getenv("PO2Q_PAIR_MW")) {
+        const int d = atoi(mv);
+        if (d >= 3 && d <= 6 && C == 16 && !residual) {
+            a.mw = 1;
+            pd = d;
+            nts = 3;
+            if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, false, pd, nts)) {
+                po2q::set_error("po2q: pair: no memory-wave plan for this shape");
+                return PO2Q_ERR_UNSUPPORTED;
+            }
+        }
+    }
     if (stg == 2 && C == 16 && !residual && W <= 4 * po2q::kABSW) {
         // role-split kernel: 2 x ceil(W / 64) waves, the pair plan's row segments
         po2q::PairABArgs b;

@@ -56,13 +56,17 @@ __device__ __forceinline__ void rows_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
 }
 template <int N>
 __device__ __forceinline__ void rows_wait() {
-    static_assert(N >= 0 && N <= 31, "vm ops issued after a row's DMAs");
+    static_assert(N >= 0 && N <= 63, "vm ops issued after a row's DMAs");
 #define PO2Q_RW(n) \
     if constexpr (N == n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory");
     PO2Q_RW(0) PO2Q_RW(1) PO2Q_RW(2) PO2Q_RW(3) PO2Q_RW(4) PO2Q_RW(5) PO2Q_RW(6) PO2Q_RW(7)
     PO2Q_RW(8) PO2Q_RW(9) PO2Q_RW(10) PO2Q_RW(11) PO2Q_RW(12) PO2Q_RW(13) PO2Q_RW(14) PO2Q_RW(15)
     PO2Q_RW(16) PO2Q_RW(17) PO2Q_RW(18) PO2Q_RW(19) PO2Q_RW(20) PO2Q_RW(21) PO2Q_RW(22) PO2Q_RW(23)
     PO2Q_RW(24) PO2Q_RW(25) PO2Q_RW(26) PO2Q_RW(27) PO2Q_RW(28) PO2Q_RW(29) PO2Q_RW(30) PO2Q_RW(31)
+    PO2Q_RW(32) PO2Q_RW(33) PO2Q_RW(34) PO2Q_RW(35) PO2Q_RW(36) PO2Q_RW(37) PO2Q_RW(38) PO2Q_RW(39)
+    PO2Q_RW(40) PO2Q_RW(41) PO2Q_RW(42) PO2Q_RW(43) PO2Q_RW(44) PO2Q_RW(45) PO2Q_RW(46) PO2Q_RW(47)
+    PO2Q_RW(48) PO2Q_RW(49) PO2Q_RW(50) PO2Q_RW(51) PO2Q_RW(52) PO2Q_RW(53) PO2Q_RW(54) PO2Q_RW(55)
+    PO2Q_RW(56) PO2Q_RW(57) PO2Q_RW(58) PO2Q_RW(59) PO2Q_RW(60) PO2Q_RW(61) PO2Q_RW(62) PO2Q_RW(63)
 #undef PO2Q_RW
 }
 

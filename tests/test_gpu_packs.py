@@ -57,7 +57,7 @@ def test_model_forward_batched_packs_bit_exact(name, image, q, bits, monkeypatch
     """The models' eval forwards: the first forward at a shape records the layers, later forwards pack
     them in batched launches up front; logits bit for bit those of the per-layer packs."""
     torch.manual_seed(0)
-    m = get_model(name, 10, quantizer_dict[q], bits, image).to(DEV).eval()
+    m = get_model(name, 10, quantizer_dict[q], bits, (image, image)).to(DEV).eval()
     x = torch.randn(4, 3, image, image, device=DEV)
     monkeypatch.setattr(qc, "BATCHED_PACKS", False)
     with torch.no_grad():
