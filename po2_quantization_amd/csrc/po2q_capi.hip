@@ -295,6 +295,10 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
         return hip_status(launch_conv_dw3(p, x, reinterpret_cast<const float*>(packed), bias, y, e.ps, e.pb, e.res,
                                           e.act, s),
                           "conv launch");
+    if (p.kind == KIND_DEPTHWISE && e.any())  // one-output-per-lane depthwise: the epilogue in its store too
+        return hip_status(launch_conv_depthwise_epi(p, x, reinterpret_cast<const float*>(packed), bias, y, e.ps, e.pb,
+                                                    e.res, e.act, s),
+                          "conv launch");
     st = hip_status(launch_conv(p, x, reinterpret_cast<const float*>(packed), bias, y, s), "conv launch");
     if (st || !e.any()) return st;
     return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, false, s), "epilogue launch");

@@ -18,6 +18,7 @@
 #include <map>
 #include <mutex>
 
+#include "po2q_epi.h"
 #include "po2q_internal.h"
 
 namespace po2q {
@@ -150,9 +151,15 @@ __global__ __launch_bounds__(kThreads) void conv_mfma_f32(const float* __restric
 }
 
 // Depthwise (groups == C, K = groups * Kg): one output element per lane.
+// EPI: the eval epilogue in the store, y = act((acc + bias) * ps[k] + pb[k] + res) (ps / pb / res
+// optional) -- the fused entry's semantics, so a depthwise layer this kernel takes (small spatial
+// sizes) needs no second elementwise pass.
+template <bool EPI>
 __global__ __launch_bounds__(kThreads) void conv_depthwise(const float* __restrict__ x, const float* __restrict__ qw,
                                                            const float* __restrict__ bias, float* __restrict__ y,
-                                                           ConvArgs a) {
+                                                           ConvArgs a, const float* __restrict__ ps,
+                                                           const float* __restrict__ pb, const float* __restrict__ res,
+                                                           int act) {
     const int64_t total = (int64_t)a.N * a.K * a.P * a.Q;
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total; idx += stride) {
@@ -175,8 +182,21 @@ __global__ __launch_bounds__(kThreads) void conv_depthwise(const float* __restri
             }
         }
         if (bias) acc += bias[k];
+        if constexpr (EPI) {
+            if (ps) acc *= ps[k];
+            if (pb) acc += pb[k];
+            if (res) acc += res[idx];
+            acc = epi_act(acc, act);
+        }
         y[idx] = acc;
     }
+}
+
+hipError_t launch_conv_depthwise_epi(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
+                                     const float* ps, const float* pb, const float* res, int act, hipStream_t s) {
+    hipLaunchKernelGGL(conv_depthwise<true>, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
+                       to_args(p), ps, pb, res, act);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ planning --
@@ -474,8 +494,8 @@ hipError_t launch_conv(const ConvPlan& p, const float* x, const float* packed, c
     if (p.kind == KIND_DEPTHWISE && p.vrx == 1)
         return launch_conv_dw3(p, x, packed, bias, y, nullptr, nullptr, nullptr, 0, s);
     if (p.kind == KIND_DEPTHWISE) {
-        hipLaunchKernelGGL(conv_depthwise, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
-                           to_args(p));
+        hipLaunchKernelGGL(conv_depthwise<false>, dim3((unsigned)p.blocks), dim3(kThreads), 0, s, x, packed, bias, y,
+                           to_args(p), nullptr, nullptr, nullptr, 0);
         return hipGetLastError();
     }
     switch (p.MI) {

@@ -42,6 +42,11 @@ hipError_t launch_conv_bf16x3_rows_epi(const ConvPlan& p, const float* x, const 
                                        const float* scale, const float* bias, float* y, const float* ps,
                                        const float* pb, int act, hipStream_t s, const WQuant& q = WQuant{});
 
+// The one-output-per-lane depthwise kernel (po2q_conv.hip, KIND_DEPTHWISE vrx 0) with the epilogue
+// in its store.
+hipError_t launch_conv_depthwise_epi(const ConvPlan& p, const float* x, const float* packed, const float* bias, float* y,
+                                     const float* ps, const float* pb, const float* res, int act, hipStream_t s);
+
 // One elementwise pass over y [N, K, PQ]: y = act(y * ps[k] + pb[k] + res) (ps / pb
 // skipped when affine_done).
 hipError_t launch_epilogue(float* y, int64_t N, int64_t K, int64_t PQ, const ConvEpi& e, bool affine_done,

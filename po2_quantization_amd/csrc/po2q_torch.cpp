@@ -504,8 +504,8 @@ at::Tensor qconv2d_chain(const at::Tensor& x_, at::TensorList weights, int64_t b
     for (int a : av) TORCH_CHECK(a >= 0 && a <= 3, "po2q: chain: unknown activation ", a);
     at::Tensor y = at::empty_like(x);
     if (x.size(0) == 0) return y;
-    const size_t wsb = po2q_qconv2d_chain_workspace_bytes(x.size(0), C, x.size(2), x.size(3), (int)n);
-    TORCH_CHECK(wsb > 0, "po2q: chain: ", last_error());
+    // 0 for a geometry the chain does not take: the entry point then reports why
+    const size_t wsb = std::max<size_t>(po2q_qconv2d_chain_workspace_bytes(x.size(0), C, x.size(2), x.size(3), (int)n), 256);
     at::Tensor ws = at::empty({(int64_t)wsb}, x.options().dtype(at::kByte));
     const int st = po2q_qconv2d_chain_f32(x.data_ptr<float>(), wp.data(), biases.size() ? bp.data() : nullptr,
                                           post_scales.size() ? sp.data() : nullptr,
