@@ -138,12 +138,13 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // the per-step barrier; the seven compute waves issue no loads, so they never wait on a vmcnt (their
 // stores are never waited for until the end).  Without it each compute wave waits, every step, for
 // its own x DMA of the previous step AND every store issued before it.  Plain / general forms
-// without a residual, seven compute waves (192 < W <= 224).
+// without a residual, seven compute waves (C = 16: 192 < W <= 224, C = 32: 96 < W <= 112); a row is
+// 14 DMA instructions either way (C x 7 * 512 / C / 4 float4).
 template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0, int MW = 0>
 __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
     static_assert(!(STG && RES), "stagger: the residual row's LDS slot is refilled before a deferred epilogue");
-    static_assert(!MW || (!RES && !STG && CC == 16), "memory wave: C = 16 forms without a residual or stagger");
+    static_assert(!MW || (!RES && !STG), "memory wave: forms without a residual or stagger");
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
     constexpr int SW = kQSW<CC>, WC = SW + 2, PL = kQPlane<CC>, KS = kQKS<CC>;
@@ -1096,7 +1097,7 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
         }
     }
 #endif
-    if constexpr (CC == 16 && PD >= 3 && (NTS == 3 || NTS == 1)) {
+    if constexpr (PD >= 3 && (NTS == 3 || NTS == 1)) {
         if (a.mw && pp.waves == 7 && !res) {  // the memory-wave kernel: 7 compute waves + 1
             const dim3 block8(64 * 8);
             if (plain)
@@ -1143,6 +1144,7 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
     PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
     PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
     PO2Q_PR(16, 3, 3) PO2Q_PR(16, 4, 3) PO2Q_PR(16, 5, 3) PO2Q_PR(16, 6, 3)
+    PO2Q_PR(32, 3, 3) PO2Q_PR(32, 4, 3) PO2Q_PR(32, 5, 3)
 #undef PO2Q_PR
     return hipErrorInvalidValue;
 }
@@ -1176,7 +1178,7 @@ void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
         if (((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) ||
-            (C == 16 && d >= 3 && d <= 6 && t == 3)) {
+            (d >= 3 && d <= (C == 16 ? 6 : 5) && t == 3)) {
             pd = d;
             nts = t;
         }
@@ -1291,7 +1293,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.mw = 0;
     if (const char* mv = getenv("PO2Q_PAIR_MW")) {
         const int d = atoi(mv);
-        if (d >= 3 && d <= 6 && C == 16 && !residual) {
+        if (d >= 3 && d <= 6 && !residual) {
             a.mw = 1;
             pd = d;
             nts = 3;

@@ -206,15 +206,18 @@ def test_pair_role_split_kernel(W, monkeypatch):
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
 
 
-@pytest.mark.parametrize("pd", [3, 4, 6])
-@pytest.mark.parametrize("shape", [(2, 23, 224), (1, 224, 224), (3, 9, 200)])
+@pytest.mark.parametrize("pd", [3, 4, 5, 6])
+@pytest.mark.parametrize("shape", [(2, 23, 224, 16), (1, 224, 224, 16), (3, 9, 200, 16), (2, 30, 112, 32),
+                                   (1, 112, 112, 32), (2, 7, 100, 32)])
 def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     """The memory-wave kernel (PO2Q_PAIR_MW = ring slots: an eighth wave issues every x DMA, the
     compute waves issue none) moves the loads, not the arithmetic: bit for bit the default kernel's
     output, plain and with the general (BN + activation) epilogue; and within the bar of torch's
     fp32 chain on Q(w)."""
-    N, H, W = shape
-    x, w1, w2, e = make(N, H, W, 41 + pd, True, 16)
+    N, H, W, C = shape
+    if C == 32 and pd > 5:
+        pytest.skip("C = 32: at most 5 ring slots fit the LDS")
+    x, w1, w2, e = make(N, H, W, 41 + pd, True, C)
     for kw in ({}, dict(act1="relu", act2="relu6", **e)):
         monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
         ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
