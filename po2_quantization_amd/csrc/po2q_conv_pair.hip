@@ -144,7 +144,13 @@ template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0
 __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
     static_assert(!(STG && RES), "stagger: the residual row's LDS slot is refilled before a deferred epilogue");
-    static_assert(!MW || (!RES && !STG), "memory wave: forms without a residual or stagger");
+    static_assert(!MW || !STG, "memory wave: no stagger");
+    // MW with RES: the residual IS x (the BasicBlock's identity shortcut, checked on the host) and is
+    // read from the x ring itself: raw row r is split at step r and re-read as output row r - 2's
+    // residual at step r + 3, so the ring keeps 4 rows behind the current one (MWL = 4) -- no
+    // residual DMAs at all.  Without RES the slot of row j - 1 is refilled at step j (MWL = 1).
+    constexpr int MWL = RES ? 4 : 1;
+    static_assert(!MW || PD - MWL - 1 >= 1, "memory wave: at least one row in flight");
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD >= 2 && PD <= 6, "raw ring slots");
     constexpr int SW = kQSW<CC>, WC = SW + 2, PL = kQPlane<CC>, KS = kQKS<CC>;
@@ -358,6 +364,8 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         const int o = j - 5;
         const bool orow = o >= 0 && o < rbe;
         const unsigned char* rres_row = resr + RS * kQResSlot;  // loaded with x row j
+        // MW: x row j - 3 (= image row p0 + o) still in the ring, [C][Wp] fp32
+        const unsigned char* rres_ring = raw + ((j + PD - 3) % PD) * rawslot + q0 * 4;
         const int g = lane >> 4;
         floatx4 vv[NT][NG];
 #pragma unroll
@@ -374,7 +382,8 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                            : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
                                     : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
                 if constexpr (RES) {
-                    const floatx4 r = *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
+                    const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * (a.Wp * 4) + ql * 4)
+                                         : *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] += r[e];
                 }
@@ -565,7 +574,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     if constexpr (MW) {
         if (wave == nw) {
 #pragma unroll
-            for (int r = 0; r < PD - 1; ++r) mw_row(r);
+            for (int r = 0; r < PD - MWL; ++r) mw_row(r);
         }
     } else {
         // x rows 0 .. PD-2, each followed by ST dropped stores (the steady-state count)
@@ -659,9 +668,9 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             // every wave finished before the barrier) takes row j + PD - 1.  Same barrier count as the
             // compute waves' loop.
             auto mstep = [&](int j) __attribute__((always_inline)) {
-                rows_wait<14 * (PD - 2)>();
+                rows_wait<14 * (PD - MWL - 1)>();  // row j landed (rows j + 1 .. j + PD - MWL - 1 may fly)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                mw_row(j + PD - 1);
+                mw_row(j + PD - MWL);  // into the slot of row j - MWL, whose last reader was step j - 1
             };
             for (int j = 0; j < nsteps; j += 6) {
                 mstep(j);
@@ -1033,7 +1042,7 @@ struct PairPlan {
     size_t lds = 0;
 };
 
-static size_t pair_lds(int C, int waves, int pd, bool res) {
+static size_t pair_lds(int C, int waves, int pd, bool res) {  // res: the compute waves' residual slots
     const int sw = 512 / C, wp = sw * waves;
     const int plane = (sw + 2) * 2 * C + 32;
     const int nf = 3 * (C == 16 ? 2 : 3) * (C / 16);
@@ -1098,8 +1107,18 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
     }
 #endif
     if constexpr (PD >= 3 && (NTS == 3 || NTS == 1)) {
-        if (a.mw && pp.waves == 7 && !res) {  // the memory-wave kernel: 7 compute waves + 1
+        if (a.mw && pp.waves == 7) {  // the memory-wave kernel: 7 compute waves + 1
             const dim3 block8(64 * 8);
+            if (res) {  // residual == x, read from the ring (checked by the caller)
+                if constexpr (PD >= 6) {
+                    if (a.act1 == 1 && a.act2 == 1)
+                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 2, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                    else
+                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                    return hipGetLastError();
+                }
+                return hipErrorInvalidValue;
+            }
             if (plain)
                 hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
             else
@@ -1293,10 +1312,12 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.mw = 0;
     if (const char* mv = getenv("PO2Q_PAIR_MW")) {
         const int d = atoi(mv);
-        if (d >= 3 && d <= 6 && !residual) {
+        // with a residual: only the identity shortcut (residual == x), from a 6-slot ring
+        const bool ring_res = residual != nullptr && residual == x && C == 16;
+        if (d >= 3 && d <= 6 && (!residual || ring_res)) {
             a.mw = 1;
-            pd = d;
-            nts = 3;
+            pd = residual ? 6 : d;
+            nts = 3;  // with the ring residual no x row is re-read from memory: non-temporal loads
             if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, false, pd, nts)) {
                 po2q::set_error("po2q: pair: no memory-wave plan for this shape");
                 return PO2Q_ERR_UNSUPPORTED;

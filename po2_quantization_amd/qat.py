@@ -156,7 +156,7 @@ class GraphedTrainStep:
         if self.graph is None:
             # eager warm-up on a side stream (po2q autotuning, lazy allocations, the optimizer's
             # momentum buffers), then every mutated tensor restored: the warm-up leaves no trace
-            before = {id(t): t.clone() for t in self._state()}
+            before = {t.data_ptr(): t.clone() for t in self._state()}  # keyed by storage: detach() is a new object
             s = torch.cuda.Stream(self.x.device)
             s.wait_stream(torch.cuda.current_stream(self.x.device))
             with torch.cuda.stream(s):
@@ -165,8 +165,8 @@ class GraphedTrainStep:
             torch.cuda.current_stream(self.x.device).wait_stream(s)
             with torch.no_grad():
                 for t in self._state():
-                    if id(t) in before:
-                        t.copy_(before[id(t)])
+                    if t.data_ptr() in before:
+                        t.copy_(before[t.data_ptr()])
                     else:  # a momentum buffer the warm-up created: zero gives SGD's first-step update
                         t.zero_()
         self.optimizer.zero_grad(set_to_none=True)
