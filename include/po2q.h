@@ -362,6 +362,31 @@ int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, con
                                  const float* residual, int act, const void* workspace,
                                  size_t workspace_bytes, void* stream);
 
+/*
+ * One whole inverted-residual block in one launch (reference models/mobilenet.py:53-134,
+ * InvertedResidual.forward :133-134; MobileViT's MV2Block, models/mobile_vit.py:131-239):
+ *   h = act1(conv(x, Q(We)) * ps1 + pb1)                      [expand; skipped when expand == NULL: h = x]
+ *   d = act2(dwconv3x3(h, Q(Wd), stride, pad 1) * ps2 + pb2)
+ *   y = act3(conv(d, Q(Wp)) * ps3 + pb3 + residual)          [residual optional: the identity shortcut]
+ * with the hidden activations h and d kept on chip.  expand / depthwise / project are the three
+ * layers' plan handles (po2q_qconv2d_plan_create: the pointwise plans must be the bf16x3
+ * pointwise kernel's, candidate index 0 of a 1x1 conv; the depthwise one a 3x3 pad-1 depthwise
+ * conv) and ws_* their workspaces with the weights already staged (po2q_qconv2d_plan_pack_batch),
+ * so Q(W) is recomputed by that pack in every forward as the reference does.  The layers are
+ * bias-free (bias=False in the reference); ps / pb are the folded eval BatchNorms (NULL: 1 / 0).
+ * Arithmetic: the pointwise plans' exact bf16x3 MFMA products and epilogue, the depthwise plan's
+ * fp32 FMAs -- the layer chain's result up to the pointwise k-split summation order.
+ * po2q_qconv2d_ir_supported: 1 when the three plans chain and a block geometry fits, 0 when not
+ * (po2q_last_error() says why; run the three layers instead), < 0 on a bad argument.
+ */
+int po2q_qconv2d_ir_supported(const po2q_conv_plan* expand, const po2q_conv_plan* depthwise,
+                              const po2q_conv_plan* project);
+int po2q_qconv2d_ir_f32(const float* x, float* y, const po2q_conv_plan* expand, const void* ws_e, size_t ws_e_bytes,
+                        const po2q_conv_plan* depthwise, const void* ws_d, size_t ws_d_bytes,
+                        const po2q_conv_plan* project, const void* ws_p, size_t ws_p_bytes, const float* ps1,
+                        const float* pb1, int act1, const float* ps2, const float* pb2, int act2, const float* ps3,
+                        const float* pb3, const float* residual, int act3, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,8 @@ EXPORTS = (
     "po2q_qconv2d_chain_supported",
     "po2q_qconv2d_chain_workspace_bytes",
     "po2q_qconv2d_chain_f32",
+    "po2q_qconv2d_ir_supported",
+    "po2q_qconv2d_ir_f32",
 )
 
 # Kernel autotuning on the first call per conv problem, the counterpart of
@@ -167,6 +169,10 @@ def load():
     L.po2q_qconv2d_plan_run_packed.argtypes = [p] * 8 + [i32, p, sz, p]
     L.po2q_qconv2d_plan_packs_weight.restype = i32
     L.po2q_qconv2d_plan_packs_weight.argtypes = [p]
+    L.po2q_qconv2d_ir_supported.restype = i32
+    L.po2q_qconv2d_ir_supported.argtypes = [p, p, p]
+    L.po2q_qconv2d_ir_f32.restype = i32
+    L.po2q_qconv2d_ir_f32.argtypes = [p, p, p, p, sz, p, p, sz, p, p, sz, p, p, i32, p, p, i32, p, p, p, i32, p]
     L.po2q_qconv2d_chain_supported.restype = i32
     L.po2q_qconv2d_chain_supported.argtypes = [i64] * 4 + [i32] * 4
     L.po2q_qconv2d_chain_workspace_bytes.restype = sz
@@ -563,42 +569,80 @@ def _layer_geometry(x_shape, stride, padding, dilation, groups):
     return [N, C, H, W, *_pair(stride), *_pair(padding), *_pair(dilation), int(groups)]
 
 
-def pack_batch(layers, bits=4, mode="po2", fsr=1, precision="auto"):
+def pack_batch(layers, bits=4, mode="po2", fsr=1, precision="auto", plans=None):
     """The weight quantize + pack of several QuantizedConv2d.forward calls (models/quantized_conv.py:35)
     as batched launches (torch.ops.po2q.qconv2d_pack_batch -> po2q_qconv2d_plan_pack_batch): layers =
     [(w, x_shape, stride, padding, dilation, groups)], all with this (bits, mode, fsr, precision).
     Returns one workspace per layer for qconv2d_packed (an empty one where the layer's kernel stages
-    its own weight).  Every layer runs the plan qconv2d() would run for it (the tuned / saved one)."""
+    its own weight).  Every layer runs the plan qconv2d() would run for it (the tuned / saved one), or
+    plans[i] when given and not None (a candidate index, as qconv2d_packed(plan=) / qconv2d_ir take)."""
     O = ops()
     if O is None:
         raise Po2qError("po2q: pack_batch needs the operator library (PO2Q_LIB selects another build)")
     mode_id, prec = MODES[mode], PRECISIONS[precision]
     geom, plans_, ws = [], [], []
-    for w, x_shape, stride, padding, dilation, groups in layers:
+    if plans is not None and len(plans) != len(layers):
+        raise Po2qError("po2q: pack_batch: one plan per layer (or none)")
+    for i, (w, x_shape, stride, padding, dilation, groups) in enumerate(layers):
         _require_hip_f32(w, "weight")
         g = _layer_geometry(x_shape, stride, padding, dilation, groups)
         geom += g
-        K, _, R, S = w.shape
-        key = tuple(g[:4]) + (int(K), int(R), int(S)) + tuple(g[4:]) + (int(bits), int(fsr), mode_id, prec)
-        saved = _saved_plan(key)
-        plans_.append(-1 if saved is None else int(saved))
+        if plans is not None and plans[i] is not None:
+            plans_.append(int(plans[i]))
+        else:
+            K, _, R, S = w.shape
+            key = tuple(g[:4]) + (int(K), int(R), int(S)) + tuple(g[4:]) + (int(bits), int(fsr), mode_id, prec)
+            saved = _saved_plan(key)
+            plans_.append(-1 if saved is None else int(saved))
         ws.append(w)
     return _op_call(O.qconv2d_pack_batch, ws, geom, int(bits), mode_id, int(fsr), prec, plans_)
 
 
 def qconv2d_packed(x, w, workspace, bias=None, stride=1, padding=0, dilation=1, groups=1, bits=4, mode="po2", fsr=1,
-                   precision="auto", post_scale=None, post_shift=None, residual=None, act="none"):
+                   precision="auto", post_scale=None, post_shift=None, residual=None, act="none", plan=None):
     """qconv2d_fused from a workspace pack_batch filled (the conv and its epilogue only; the weight
-    was quantized + packed by the batched launch).  Bit for bit qconv2d_fused's result."""
+    was quantized + packed by the batched launch).  Bit for bit qconv2d_fused's result.  plan: the
+    candidate index the workspace was packed for (None: the tuned / saved plan, as pack_batch)."""
     O = ops()
     if O is None:
         raise Po2qError("po2q: qconv2d_packed needs the operator library (PO2Q_LIB selects another build)")
     xc, wc, bc, args, yshape = _conv_geometry(x, w, bias, stride, padding, dilation, groups)
     key = args + (int(bits), int(fsr), MODES[mode], PRECISIONS[precision])
-    saved = _saved_plan(key)
+    saved = _saved_plan(key) if plan is None else int(plan)
     return _op_call(O.qconv2d_packed, xc, wc, workspace, bc, list(args[7:9]), list(args[9:11]), list(args[11:13]),
                     args[13], int(bits), MODES[mode], int(fsr), PRECISIONS[precision], -1 if saved is None else int(saved),
                     post_scale, post_shift, residual, ACTS[act])
+
+
+def qconv2d_ir(x, we, wd, wp, ws_e, ws_d, ws_p, stride=1, bits=4, mode="po2", fsr=1, precision="auto",
+               ps1=None, pb1=None, act1="relu6", ps2=None, pb2=None, act2="relu6", ps3=None, pb3=None,
+               residual=None, act3="none", plans=(0, 0, 0)):
+    """One inverted-residual block (reference mobilenet.py:53-134: expand 1x1 -> BN -> act ->
+    depthwise 3x3 -> BN -> act -> project 1x1 -> BN (+ x); we = None: no expand) in ONE launch
+    (torch.ops.po2q.qconv2d_ir -> po2q_qconv2d_ir_f32) from the three layers' workspaces filled by
+    pack_batch (ws_e None without expand).  The hidden activations stay on chip; the result is the
+    three qconv2d_packed calls' up to the pointwise kernels' k-split summation order.  Shapes the
+    fused kernel does not take run as those three calls.  plans: the candidate index each workspace was
+    packed for (pack_batch(plans=)); the default 0 is each layer's heuristic plan (the pointwise and
+    depthwise kernels whose packs the block kernel reads), None entries the tuned / saved plan."""
+    O = ops()
+    if O is None:
+        raise Po2qError("po2q: qconv2d_ir needs the operator library (PO2Q_LIB selects another build)")
+    _require_hip_f32(x, "input")
+    N, Cin, H, W = (int(v) for v in x.shape)
+    Ch, Cout, s = int(wd.shape[0]), int(wp.shape[0]), int(stride)
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    mode_id, prec = MODES[mode], PRECISIONS[precision]
+    tail = (int(bits), int(fsr), mode_id, prec)
+    keys = [(N, Cin, H, W, Ch, 1, 1, 1, 1, 0, 0, 1, 1, 1) + tail if we is not None else None,
+            (N, Ch, H, W, Ch, 3, 3, s, s, 1, 1, 1, 1, Ch) + tail,
+            (N, Ch, Ho, Wo, Cout, 1, 1, 1, 1, 0, 0, 1, 1, 1) + tail]
+    plans_ = []
+    for k, pl in zip(keys, plans):
+        saved = (_saved_plan(k) if k is not None else None) if pl is None else pl
+        plans_.append(-1 if saved is None else int(saved))
+    return _op_call(O.qconv2d_ir, x, we, wd, wp, ws_e, ws_d, ws_p, s, int(bits), mode_id, int(fsr), prec, ps1, pb1,
+                    ACTS[act1], ps2, pb2, ACTS[act2], ps3, pb3, residual, ACTS[act3], plans_)
 
 
 class PackedConvs:

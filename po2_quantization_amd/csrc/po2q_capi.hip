@@ -676,6 +676,97 @@ int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, con
                     workspace_bytes, reinterpret_cast<hipStream_t>(stream), e, RUN_CONV);
 }
 
+// ------------------------------------------------------------------ inverted-residual block --
+// The three plans of one block: expand (optional) 1x1 pointwise, depthwise 3x3 pad 1, project
+// 1x1 pointwise, chained shapes, each plan's weight staged in its workspace (the pointwise
+// packs and the depthwise plain copy).  Fills the block geometry; 0 or an error with the reason.
+static int ir_check(const po2q_conv_plan* e, const po2q_conv_plan* d, const po2q_conv_plan* p, po2q::IrPlan* ip,
+                    int64_t* shape) {
+    using namespace po2q;
+    if (!d || !p) {
+        set_error("po2q: inverted residual: null depthwise or project plan");
+        return PO2Q_ERR_INVALID;
+    }
+    auto pointwise = [](const ConvPlan& q) {
+        return q.kind == KIND_BF16X3_PW && !q.fp && q.R == 1 && q.S == 1 && q.sh == 1 && q.sw == 1 && q.ph == 0 &&
+               q.pw == 0 && q.groups == 1;
+    };
+    const ConvPlan& D = d->p;
+    const ConvPlan& Pj = p->p;
+    const int64_t N = D.N, Ch = D.C, H = D.H, W = D.W, S = D.sh;
+    std::string why;
+    if (D.kind != KIND_DEPTHWISE || D.groups != D.C || D.K != D.C || D.R != 3 || D.S != 3 || D.sh != D.sw ||
+        D.ph != 1 || D.pw != 1 || D.dh != 1 || D.dw != 1)
+        why = "the depthwise plan is not a 3x3 pad-1 depthwise conv";
+    else if (!pointwise(Pj) || Pj.N != N || Pj.C != Ch || Pj.H != D.P || Pj.W != D.Q)
+        why = "the project plan is not a pointwise bf16x3 conv of the depthwise output";
+    else if (e && (!pointwise(e->p) || e->p.N != N || e->p.K != Ch || e->p.H != H || e->p.W != W))
+        why = "the expand plan is not a pointwise bf16x3 conv producing the depthwise input";
+    else if ((e && e->mode == PO2Q_MODE_NONE) || d->mode == PO2Q_MODE_NONE || p->mode == PO2Q_MODE_NONE)
+        why = "mode none has no staged weights";
+    const int64_t Cin = e ? e->p.C : Ch;
+    if (why.empty() && !ir_plan(*ip, N, Cin, H, W, Ch, Pj.K, S, e != nullptr))
+        why = "no block geometry fits (channels not a multiple of 16, or too large)";
+    if (!why.empty()) {
+        set_error("po2q: inverted residual: " + why);
+        return PO2Q_ERR_UNSUPPORTED;
+    }
+    if (shape) {
+        shape[0] = N; shape[1] = Cin; shape[2] = H; shape[3] = W; shape[4] = Ch; shape[5] = Pj.K; shape[6] = S;
+    }
+    return PO2Q_OK;
+}
+
+int po2q_qconv2d_ir_supported(const po2q_conv_plan* expand, const po2q_conv_plan* depthwise,
+                              const po2q_conv_plan* project) {
+    po2q::IrPlan ip;
+    const int st = ir_check(expand, depthwise, project, &ip, nullptr);
+    if (st == PO2Q_OK) return 1;
+    return st == PO2Q_ERR_UNSUPPORTED ? 0 : -st;
+}
+
+int po2q_qconv2d_ir_f32(const float* x, float* y, const po2q_conv_plan* expand, const void* ws_e, size_t ws_e_bytes,
+                        const po2q_conv_plan* depthwise, const void* ws_d, size_t ws_d_bytes,
+                        const po2q_conv_plan* project, const void* ws_p, size_t ws_p_bytes, const float* ps1,
+                        const float* pb1, int act1, const float* ps2, const float* pb2, int act2, const float* ps3,
+                        const float* pb3, const float* residual, int act3, void* stream) {
+    using namespace po2q;
+    if (!x || !y || !ws_d || !ws_p || (expand && !ws_e)) {
+        set_error("po2q: inverted residual: null pointer");
+        return PO2Q_ERR_INVALID;
+    }
+    for (int a : {act1, act2, act3})
+        if (a < PO2Q_ACT_NONE || a > PO2Q_ACT_SILU) {
+            set_error("po2q: unknown activation " + std::to_string(a));
+            return PO2Q_ERR_INVALID;
+        }
+    IrPlan ip;
+    int64_t sh[7];
+    int st = ir_check(expand, depthwise, project, &ip, sh);
+    if (st) return st;
+    const po2q_conv_plan* hs[3] = {expand, depthwise, project};
+    const void* wss[3] = {ws_e, ws_d, ws_p};
+    const size_t wsb[3] = {ws_e_bytes, ws_d_bytes, ws_p_bytes};
+    const char* at[3] = {nullptr, nullptr, nullptr};  // staged weights
+    const float* sc[3] = {nullptr, nullptr, nullptr};
+    for (int i = 0; i < 3; ++i) {
+        if (!hs[i]) continue;
+        const WsLayout L = ws_layout(hs[i]->p, hs[i]->mode);
+        if (wsb[i] < L.total) {
+            set_error("po2q: inverted residual: workspace too small (need " + std::to_string(L.total) + " bytes)");
+            return PO2Q_ERR_WORKSPACE;
+        }
+        at[i] = reinterpret_cast<const char*>(wss[i]) + L.packed_off;
+        sc[i] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(wss[i]) + L.scale_off);
+    }
+    const IrEpi ep{ps1, pb1, ps2, pb2, ps3, pb3, act1, act2, act3, residual};
+    return hip_status(launch_conv_ir(ip, x, y, (int)sh[0], (int)sh[1], (int)sh[2], (int)sh[3], (int)sh[4], (int)sh[5],
+                                     (int)sh[6], reinterpret_cast<const uint16_t*>(at[0]), sc[0],
+                                     reinterpret_cast<const float*>(at[1]), reinterpret_cast<const uint16_t*>(at[2]),
+                                     sc[2], ep, reinterpret_cast<hipStream_t>(stream)),
+                      "inverted residual launch");
+}
+
 int po2q_qconv2d_plan_describe(const po2q_conv_plan* plan, char* buf, size_t len) {
     if (!plan || !buf || len == 0) {
         po2q::set_error("po2q: null plan or buffer");

@@ -1,0 +1,335 @@
+// A whole MobileNetV2 inverted-residual block in ONE launch (reference models/mobilenet.py:53-134;
+// MobileViT's MV2Block has the same shape, models/mobile_vit.py:131-239): three QuantizedConv2d
+// forwards (quantized_conv.py:32-38) with their eval BatchNorms and activations,
+//     h = act1(bn1(conv1x1(x, Q(We))))          expand (absent when the expand ratio is 1: h = x)
+//     d = act2(bn2(dwconv3x3(h, Q(Wd), stride, pad 1)))
+//     y = act3(bn3(conv1x1(d, Q(Wp))) (+ x))    project; the identity shortcut when stride 1, Cin == Cout
+// The hidden activations h and d never leave the CU.
+//
+// Why: at CIFAR size every layer of MobileNetV2 is a few MB of activations and a few microseconds
+// of work, so the layer-by-layer forward is ~50 latency-bound launches whose HBM traffic is
+// dominated by the 6x-wide hidden tensors (written by the expand, read + written by the depthwise,
+// read by the project).  Here a block owns a band of R output rows of G images (G > 1 only when
+// one image is one band) and walks the hidden channels in chunks of CHK (a multiple of 32):
+//   prologue   the band's input rows (+ the depthwise halo) of x -> LDS fp32 [pixel][Cin + pad];
+//   per chunk  expand: (16-pixel group, pair of 16-channel tiles) units on v_mfma_f32_16x16x32_bf16
+//              (A = the exact hi / mid / lo bf16 split of x, B = the expand layer's pointwise
+//              pack), bn1 + act1 -> hidden fp32 [channel][pixel];  barrier;
+//              depthwise 3x3: fp32 FMAs in conv_dw3's tap order (the quantized depthwise weight
+//              is exact fp32), bn2 + act2, exact split -> bf16 planes [output pixel][CHK];
+//              barrier;
+//              project: every wave accumulates its (output-pixel group, output-channel tile)
+//              units over the chunk's k-steps (B = the project layer's pointwise pack);
+//   epilogue   bn3 (+ the residual x) + act3 -> y.
+// Weights come from the three layers' own packs (qconv2d_pack_batch: the pointwise [ks][nt][lane]
+// bf16 fragments + scale multiplier, the depthwise plain quantized fp32 copy), so every weight is
+// still quantized in every forward.  Arithmetic per layer is the layer kernels' own (conv_pw's
+// MFMA order and epilogue expression, conv_dw3's fma order and epilogue), so the block equals
+// the layer chain up to the pointwise kernels' k-split summation order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "po2q_epi.h"
+#include "po2q_internal.h"
+#include "po2q_x3_dev.h"
+
+namespace po2q {
+
+namespace {
+constexpr int kIrThreads = 512;  // 8 waves
+constexpr int kIrWaves = kIrThreads / 64;
+constexpr int kIrUnits = 8;  // project units (output-pixel group x output-channel tile) per wave
+constexpr size_t kIrLds = 150 * 1024;
+}  // namespace
+
+struct IrArgs {
+    int N, Cin, H, W, Ch, Cout, S, Ho, Wo;
+    int G, R, RI, nbands;  // images per block, output / input rows per band, bands per image
+    int CHK;               // hidden channels per chunk (multiple of 32)
+    int KSe, NTe, NTp;     // expand k-steps (32 ch), expand / project 16-channel output tiles
+    int xs;                // x row stride in LDS (floats): 32 KSe + 4
+    int P, PG, Po, HP;     // input pixels, their 16-groups, output pixels (x16) of a block; hidden row stride
+    const uint4* we;       // expand pack (NULL: h = x)
+    const float* we_scale;
+    const float* wd;  // depthwise quantized weight [Ch][9]
+    const uint4* wp;  // project pack
+    const float* wp_scale;
+    const float *ps1, *pb1, *ps2, *pb2, *ps3, *pb3;
+    int act1, act2, act3;
+    const float* res;      // residual [N, Cout, Ho, Wo] or NULL
+    int off_hid, off_dpl;  // LDS byte offsets
+};
+
+// LDS: x [16 PG][xs] fp32 (expand only) | hidden chunk [CHK][HP] fp32 | d planes 3 x [Po][CHK] bf16
+__global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ x, float* __restrict__ y, IrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, pl = lane & 15;
+    const int band = blockIdx.x % a.nbands, n0 = (blockIdx.x / a.nbands) * a.G;
+    const int oy0 = band * a.R, Rb = min(a.R, a.Ho - oy0);
+    const int iy0 = max(0, oy0 * a.S - 1), iy1 = min(a.H - 1, (oy0 + Rb - 1) * a.S + 1);
+    const int IMG = a.RI * a.W, IMGo = a.R * a.Wo;  // LDS pixels of one image (input / output)
+    const bool expand = a.we != nullptr;
+    float* xl = reinterpret_cast<float*>(lds);
+    float* hid = reinterpret_cast<float*>(lds + a.off_hid);
+    unsigned char* dpl = lds + a.off_dpl;
+    const int drow = a.CHK * 2;        // bytes per output pixel of a d plane
+    const int dplane = a.Po * drow;    // bytes per d plane
+
+    // the band's input pixel px (image, row iy0 + ry, column) of channel c; 0 outside
+    auto x_at = [&](int c, int px) -> float {
+        const int img = px / IMG, r = px - img * IMG;
+        const int ry = r / a.W, ix = r - ry * a.W;
+        const int iy = iy0 + ry;
+        if (img >= a.G || n0 + img >= a.N || iy > iy1 || c >= a.Cin) return 0.0f;
+        return x[(((int64_t)(n0 + img) * a.Cin + c) * a.H + iy) * a.W + ix];
+    };
+
+    if (expand) {
+        const int cinp = 32 * a.KSe, P16 = 16 * a.PG;
+        for (int u = tid; u < P16 * cinp; u += kIrThreads) {
+            const int c = u / P16, px = u - c * P16;
+            xl[px * a.xs + c] = x_at(c, px);
+        }
+    }
+    const float se = expand ? *a.we_scale : 1.0f;
+    const float sp = *a.wp_scale;
+
+    const int nunits = a.Po / 16 * a.NTp;
+    floatx4 acc[kIrUnits];
+#pragma unroll
+    for (int i = 0; i < kIrUnits; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c0 = 0; c0 < a.Ch; c0 += a.CHK) {
+        const int CH = min(a.CHK, a.Ch - c0);  // a multiple of 16
+        __syncthreads();  // x staged / the previous chunk's depthwise reads of hid retired
+        // ---- expand (or copy x) -> hid [CH][HP] fp32
+        if (expand) {
+            const int ntile = CH / 16, npair = (ntile + 1) / 2;
+            for (int u = wave; u < a.PG * npair; u += kIrWaves) {
+                const int pg = u / npair, tp = u - pg * npair;
+                const int t0 = 2 * tp, nt = min(2, ntile - t0);
+                floatx4 c[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+                const float* xr = xl + (16 * pg + pl) * a.xs + 8 * g;
+                for (int ks = 0; ks < a.KSe; ++ks) {
+                    const floatx4 v0 = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
+                    const floatx4 v1 = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+                    const uint32_t b[8] = {__float_as_uint(v0[0]), __float_as_uint(v0[1]), __float_as_uint(v0[2]),
+                                           __float_as_uint(v0[3]), __float_as_uint(v1[0]), __float_as_uint(v1[1]),
+                                           __float_as_uint(v1[2]), __float_as_uint(v1[3])};
+                    uint4 hi, mid, lo;
+                    split3(b, hi, mid, lo);
+                    const bf16x8 ah = __builtin_bit_cast(bf16x8, hi), am = __builtin_bit_cast(bf16x8, mid),
+                                 al = __builtin_bit_cast(bf16x8, lo);
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        if (t < nt) {  // wave-uniform
+                            const int tile = c0 / 16 + t0 + t;
+                            const bf16x8 bw = __builtin_bit_cast(bf16x8, a.we[((int64_t)ks * a.NTe + tile) * 64 + lane]);
+                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, c[t], 0, 0, 0);
+                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, c[t], 0, 0, 0);
+                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, c[t], 0, 0, 0);
+                        }
+                    }
+                }
+                // lane: hidden channel c0 + 16 (t0 + t) + pl, pixels 16 pg + 4 g .. + 3 (conv_pw's epilogue)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    if (t >= nt) break;
+                    const int hc = 16 * (t0 + t) + pl, h = c0 + hc;
+                    const float s1 = a.ps1 ? a.ps1[h] : 1.0f, b1 = a.pb1 ? a.pb1[h] : 0.0f;
+                    floatx4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float q = c[t][e] * se + 0.0f;
+                        q = q * s1 + b1;
+                        v[e] = epi_act(q, a.act1);
+                    }
+                    *reinterpret_cast<floatx4*>(hid + hc * a.HP + 16 * pg + 4 * g) = v;
+                }
+            }
+        } else {
+            for (int u = tid; u < CH * a.P; u += kIrThreads) {
+                const int hc = u / a.P, px = u - hc * a.P;
+                hid[hc * a.HP + px] = x_at(c0 + hc, px);
+            }
+        }
+        __syncthreads();
+        // ---- depthwise 3x3 (pad 1, stride S), bn2 + act2, split -> d planes [Po][CHK]
+        const int noct = a.CHK / 8;
+        for (int u = tid; u < a.Po * noct; u += kIrThreads) {
+            const int oc = u / a.Po, op = u - oc * a.Po;
+            const int img = op / IMGo, r = op - img * IMGo;
+            const int ry = r / a.Wo, ox = r - ry * a.Wo;
+            const int oy = oy0 + ry;
+            const bool ok = img < a.G && ry < Rb;
+            uint32_t b[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int hc = 8 * oc + e;
+                float v = 0.0f;
+                if (ok && hc < CH) {
+                    const int h = c0 + hc;
+                    const float* wk = a.wd + h * 9;
+                    const float* hp = hid + hc * a.HP + img * IMG;
+                    float s = 0.0f;
+#pragma unroll
+                    for (int rr = 0; rr < 3; ++rr) {
+                        const int iy = oy * a.S - 1 + rr;
+                        const bool rok = iy >= 0 && iy < a.H;
+#pragma unroll
+                        for (int t = 0; t < 3; ++t) {
+                            const int ix = ox * a.S - 1 + t;
+                            const float hv = (rok && ix >= 0 && ix < a.W) ? hp[(iy - iy0) * a.W + ix] : 0.0f;
+                            s = fmaf(hv, wk[rr * 3 + t], s);
+                        }
+                    }
+                    float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
+                    q = q * (a.ps2 ? a.ps2[h] : 1.0f) + (a.pb2 ? a.pb2[h] : 0.0f);
+                    v = epi_act(q, a.act2);
+                }
+                b[e] = __float_as_uint(v);
+            }
+            uint4 hi, mid, lo;
+            split3(b, hi, mid, lo);
+            const int off = op * drow + 16 * oc;
+            *reinterpret_cast<uint4*>(dpl + off) = hi;
+            *reinterpret_cast<uint4*>(dpl + dplane + off) = mid;
+            *reinterpret_cast<uint4*>(dpl + 2 * dplane + off) = lo;
+        }
+        __syncthreads();
+        // ---- project: the chunk's k-steps into this wave's units
+        const int nks = (CH + 31) / 32;
+#pragma unroll
+        for (int i = 0; i < kIrUnits; ++i) {
+            const int u = wave + kIrWaves * i;
+            if (u >= nunits) break;
+            const int opg = u / a.NTp, ot = u - opg * a.NTp;
+            for (int k2 = 0; k2 < nks; ++k2) {
+                const int ks = c0 / 32 + k2;
+                const bf16x8 bw = __builtin_bit_cast(bf16x8, a.wp[((int64_t)ks * a.NTp + ot) * 64 + lane]);
+                const int off = (16 * opg + pl) * drow + 16 * (4 * k2 + g);
+#pragma unroll
+                for (int p3 = 0; p3 < 3; ++p3) {
+                    const bf16x8 af =
+                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(dpl + p3 * dplane + off));
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[i], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---- epilogue (conv_pw's): lane holds output channel 16 ot + pl, output pixels 16 opg + 4 g .. + 3
+#pragma unroll
+    for (int i = 0; i < kIrUnits; ++i) {
+        const int u = wave + kIrWaves * i;
+        if (u >= nunits) break;
+        const int opg = u / a.NTp, ot = u - opg * a.NTp;
+        const int k = 16 * ot + pl;
+        if (k >= a.Cout) continue;
+        const float s3 = a.ps3 ? a.ps3[k] : 1.0f, b3 = a.pb3 ? a.pb3[k] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int op = 16 * opg + 4 * g + e;
+            const int img = op / IMGo, r = op - img * IMGo;
+            const int ry = r / a.Wo, ox = r - ry * a.Wo;
+            if (img >= a.G || n0 + img >= a.N || ry >= Rb) continue;
+            const int64_t yi = (((int64_t)(n0 + img) * a.Cout + k) * a.Ho + oy0 + ry) * a.Wo + ox;
+            float v = acc[i][e] * sp + 0.0f;
+            v = v * s3 + b3;
+            if (a.res) v += a.res[yi];
+            y[yi] = epi_act(v, a.act3);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ planning --
+namespace {
+
+bool ir_geom(IrPlan& q, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout, int64_t S, bool expand,
+             int64_t R, int64_t G, int64_t CHK) {
+    const int64_t Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+    const int64_t RI = std::min<int64_t>(H, (R - 1) * S + 3);
+    const int64_t P = G * RI * W, PG = (P + 15) / 16, Po = (G * R * Wo + 15) / 16 * 16;
+    const int64_t xs = 32 * ((Cin + 31) / 32) + 4;
+    const int64_t HP = 16 * PG + 4;  // 16-byte shift between channel rows: conflict-free float4 stores
+    const size_t xb = expand ? (size_t)16 * PG * xs * 4 : 0;
+    const size_t hb = (size_t)CHK * HP * 4;
+    const size_t db = (size_t)3 * Po * CHK * 2;
+    if (xb + hb + db > kIrLds) return false;
+    if (Po / 16 * ((Cout + 15) / 16) > kIrWaves * kIrUnits) return false;
+    q.G = (int)G; q.R = (int)R; q.RI = (int)RI; q.nbands = (int)((Ho + R - 1) / R); q.CHK = (int)CHK;
+    q.P = (int)P; q.PG = (int)PG; q.Po = (int)Po; q.HP = (int)HP; q.xs = (int)xs;
+    q.lds = xb + hb + db; q.off_hid = xb; q.off_dpl = xb + hb;
+    (void)Ch;
+    return true;
+}
+
+}  // namespace
+
+// Geometry: whole images when one fits (G > 1 of them while a block has < 64 output pixels and
+// the grid keeps >= 512 blocks), else the tallest band of one image that fits the LDS budget and
+// the project unit cap; then the widest hidden chunk (up to 256 channels, no wider than the
+// hidden width) that still fits: small images get few, wide chunks (fewer barriers).
+bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout, int64_t S,
+             bool expand) {
+    if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Ch <= 0 || Cout <= 0 || (S != 1 && S != 2)) return false;
+    if (Ch % 16 != 0 || (!expand && Ch != Cin) || Cin > 1024 || Ch > 4096 || Cout > 1024) return false;
+    if (N * Cin * H * W >= INT32_MAX || N * Cout * H * W >= INT32_MAX || N * Ch * H * W >= ((int64_t)1 << 40))
+        return false;
+    const int64_t Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+    IrPlan q{};
+    bool found = false;
+    int64_t R = Ho, G = 1;
+    for (; R >= 1 && !found; --R) found = ir_geom(q, Cin, H, W, Ch, Cout, S, expand, R, 1, 32);
+    if (!found) return false;
+    R = q.R;
+    if (R == Ho) {
+        while (G * Ho * Wo < 64 && N / (G * 2) >= 512) {
+            IrPlan q2{};
+            if (!ir_geom(q2, Cin, H, W, Ch, Cout, S, expand, R, G * 2, 32)) break;
+            q = q2;
+            G *= 2;
+        }
+    }
+    // the widest chunk that fits (q holds the 32-channel geometry, which does)
+    const int64_t chmax = (Ch + 31) / 32 * 32;
+    for (int64_t CHK = std::min<int64_t>(256, chmax); CHK > 32; CHK -= 32)
+        if (ir_geom(q, Cin, H, W, Ch, Cout, S, expand, R, G, CHK)) break;
+    ip = q;
+    ip.blocks = (N + G - 1) / G * q.nbands;
+    return true;
+}
+
+hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int Cin, int H, int W, int Ch, int Cout,
+                          int S, const uint16_t* we, const float* we_scale, const float* wd, const uint16_t* wp,
+                          const float* wp_scale, const IrEpi& e, hipStream_t s) {
+    IrArgs a;
+    a.N = N; a.Cin = Cin; a.H = H; a.W = W; a.Ch = Ch; a.Cout = Cout; a.S = S;
+    a.Ho = (H - 1) / S + 1; a.Wo = (W - 1) / S + 1;
+    a.G = ip.G; a.R = ip.R; a.RI = ip.RI; a.nbands = ip.nbands; a.CHK = ip.CHK;
+    a.KSe = (Cin + 31) / 32; a.NTe = (Ch + 15) / 16; a.NTp = (Cout + 15) / 16;
+    a.xs = ip.xs; a.P = ip.P; a.PG = ip.PG; a.Po = ip.Po; a.HP = ip.HP;
+    a.we = reinterpret_cast<const uint4*>(we);
+    a.we_scale = we_scale;
+    a.wd = wd;
+    a.wp = reinterpret_cast<const uint4*>(wp);
+    a.wp_scale = wp_scale;
+    a.ps1 = e.ps1; a.pb1 = e.pb1; a.ps2 = e.ps2; a.pb2 = e.pb2; a.ps3 = e.ps3; a.pb3 = e.pb3;
+    a.act1 = e.act1; a.act2 = e.act2; a.act3 = e.act3;
+    a.res = e.res;
+    a.off_hid = (int)ip.off_hid;
+    a.off_dpl = (int)ip.off_dpl;
+    if (ip.lds > 64 * 1024) {
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv_ir),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kIrLds);
+        if (attr != hipSuccess) return attr;
+    }
+    hipLaunchKernelGGL(conv_ir, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
+    return hipGetLastError();
+}
+
+}  // namespace po2q

@@ -191,6 +191,26 @@ hipError_t launch_conv_bf16x3_rows(const ConvPlan& p, const float* x, const uint
 hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint16_t* packed,
                                   const float* scale, const float* bias, float* y, hipStream_t s);
 
+// Fused inverted-residual block (po2q_conv_ir.hip): expand 1x1 -> depthwise 3x3 -> project 1x1 with
+// eval BN / activations / identity residual, hidden activations in LDS.
+struct IrPlan {
+    int G, R, RI, nbands, CHK, P, PG, Po, HP, xs;
+    size_t lds, off_hid, off_dpl;
+    int64_t blocks;
+};
+struct IrEpi {
+    const float *ps1, *pb1, *ps2, *pb2, *ps3, *pb3;  // each optional (NULL)
+    int act1, act2, act3;
+    const float* res;  // residual [N, Cout, Ho, Wo] or NULL
+};
+bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout, int64_t S,
+             bool expand);
+// we / we_scale: the expand layer's pointwise (KIND_BF16X3_PW) pack, NULL when there is no expand;
+// wd: the depthwise plain quantized copy [Ch][9]; wp / wp_scale: the project layer's pointwise pack.
+hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int Cin, int H, int W, int Ch, int Cout,
+                          int S, const uint16_t* we, const float* we_scale, const float* wd, const uint16_t* wp,
+                          const float* wp_scale, const IrEpi& e, hipStream_t s);
+
 // fp64 / bf16 (bit patterns) PO2 / PO2+ quantizer (po2q_quant_dtypes.hip): absmax partials
 // (nparts = absmax_blocks(n) uint64 words), then the quantize pass.
 template <typename T>

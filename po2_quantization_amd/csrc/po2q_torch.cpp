@@ -22,6 +22,9 @@
 //                        the weight quantize of every QuantizedConv2d.forward of a model forward
 //                        (quantized_conv.py:35) as batched launches, then each conv (+ epilogue)
 //                        from its packed workspace
+//   po2q::qconv2d_ir     a whole inverted-residual block (expand 1x1 -> depthwise 3x3 -> project
+//                        1x1, BN / ReLU6 / identity shortcut) in one launch from the three layers'
+//                        packed workspaces (mobilenet.py:53-134, mobile_vit.py:131-239)
 // Meta kernels give the output shapes (FX / torch.compile tracing, fake tensors).
 // Errors are TORCH_CHECK -> RuntimeError, as F.conv2d raises for bad arguments.
 #include <ATen/ATen.h>
@@ -641,6 +644,122 @@ at::Tensor qconv2d_packed_meta(const at::Tensor& x, const at::Tensor& w, const a
     return qconv2d_meta(x, w, bias, stride, padding, dilation, groups, bits, mode, fsr, prec, plan, 0);
 }
 
+// ---- one inverted-residual block (expand -> depthwise 3x3 -> project) from packed workspaces ----
+// we / ws_e absent: no expand (h = x).  The workspaces come from qconv2d_pack_batch with the
+// same geometry and plan indices (plans: 3 ints, or empty for -1 = tuned / heuristic).  When the
+// three plans cannot run as one block (po2q_qconv2d_ir_supported) or a workspace is empty the
+// three layers run one by one from their workspaces (qconv2d_packed) -- the same HIP kernels.
+struct IrShape {
+    int64_t N, Cin, H, W, Ch, Cout, S, Ho, Wo;
+};
+
+IrShape ir_shape(const at::Tensor& x, const c10::optional<at::Tensor>& we, const at::Tensor& wd, const at::Tensor& wp,
+                 int64_t stride) {
+    TORCH_CHECK(x.dim() == 4, "po2q: inverted residual: x must be 4-D [N, C, H, W]");
+    TORCH_CHECK(stride == 1 || stride == 2, "po2q: inverted residual: stride must be 1 or 2");
+    IrShape s{x.size(0), x.size(1), x.size(2), x.size(3), wd.size(0), wp.size(0), stride, 0, 0};
+    TORCH_CHECK(wd.dim() == 4 && wd.size(1) == 1 && wd.size(2) == 3 && wd.size(3) == 3,
+                "po2q: inverted residual: the depthwise weight must be [Ch, 1, 3, 3], got ", wd.sizes());
+    if (we.has_value()) {
+        TORCH_CHECK(we->dim() == 4 && we->size(0) == s.Ch && we->size(1) == s.Cin && we->size(2) == 1 &&
+                        we->size(3) == 1,
+                    "po2q: inverted residual: the expand weight must be [Ch, Cin, 1, 1] = [", s.Ch, ", ", s.Cin,
+                    ", 1, 1], got ", we->sizes());
+    } else {
+        TORCH_CHECK(s.Cin == s.Ch, "po2q: inverted residual without expand: x has ", s.Cin,
+                    " channels, the depthwise conv ", s.Ch);
+    }
+    TORCH_CHECK(wp.dim() == 4 && wp.size(1) == s.Ch && wp.size(2) == 1 && wp.size(3) == 1,
+                "po2q: inverted residual: the project weight must be [Cout, Ch, 1, 1], got ", wp.sizes());
+    s.Ho = (s.H - 1) / stride + 1;
+    s.Wo = (s.W - 1) / stride + 1;
+    return s;
+}
+
+at::Tensor qconv2d_ir(const at::Tensor& x_, const c10::optional<at::Tensor>& we, const at::Tensor& wd,
+                      const at::Tensor& wp, const c10::optional<at::Tensor>& ws_e, const at::Tensor& ws_d,
+                      const at::Tensor& ws_p, int64_t stride, int64_t bits, int64_t mode, int64_t fsr, int64_t prec,
+                      const c10::optional<at::Tensor>& ps1, const c10::optional<at::Tensor>& pb1, int64_t act1,
+                      const c10::optional<at::Tensor>& ps2, const c10::optional<at::Tensor>& pb2, int64_t act2,
+                      const c10::optional<at::Tensor>& ps3, const c10::optional<at::Tensor>& pb3,
+                      const c10::optional<at::Tensor>& residual, int64_t act3, at::IntArrayRef plans) {
+    check_hip_f32(x_, "x");
+    check_hip_f32(wd, "depthwise weight");
+    check_hip_f32(wp, "project weight");
+    if (we.has_value()) check_hip_f32(*we, "expand weight");
+    const IrShape s = ir_shape(x_, we, wd, wp, stride);
+    TORCH_CHECK(plans.empty() || plans.size() == 3, "po2q: inverted residual: 3 plan indices (or none)");
+    TORCH_CHECK(we.has_value() == ws_e.has_value(), "po2q: inverted residual: ws_e goes with we");
+    for (int64_t a : {act1, act2, act3}) TORCH_CHECK(a >= 0 && a <= 3, "po2q: unknown activation ", a);
+    const int64_t pe = plans.empty() ? -1 : plans[0], pd = plans.empty() ? -1 : plans[1],
+                  pp = plans.empty() ? -1 : plans[2];
+    const bool have_ws = (!ws_e.has_value() || ws_e->numel() > 0) && ws_d.numel() > 0 && ws_p.numel() > 0;
+    const DeviceGuard guard(x_.device());
+    const int64_t dev = x_.device().index();
+    PlanEntry* ee = we.has_value()
+                        ? plan_lookup({s.N, s.Cin, s.H, s.W, s.Ch, 1, 1, 1, 1, 0, 0, 1, 1, 1}, bits, fsr, mode, prec, pe, dev)
+                        : nullptr;
+    PlanEntry* ed = plan_lookup({s.N, s.Ch, s.H, s.W, s.Ch, 3, 3, s.S, s.S, 1, 1, 1, 1, s.Ch}, bits, fsr, mode, prec,
+                                pd, dev);
+    PlanEntry* ep = plan_lookup({s.N, s.Ch, s.Ho, s.Wo, s.Cout, 1, 1, 1, 1, 0, 0, 1, 1, 1}, bits, fsr, mode, prec, pp,
+                                dev);
+    const int sup = have_ws ? po2q_qconv2d_ir_supported(ee ? ee->plan : nullptr, ed->plan, ep->plan) : 0;
+    TORCH_CHECK(sup >= 0, last_error());
+    if (sup == 0 || s.N == 0) {  // the layer chain from the same workspaces
+        const at::Tensor empty = at::empty({0}, x_.options().dtype(at::kByte));
+        at::Tensor h = x_;
+        if (we.has_value())
+            h = qconv2d_packed(x_, *we, ws_e->numel() ? *ws_e : empty, c10::nullopt, {1, 1}, {0, 0}, {1, 1}, 1, bits,
+                               mode, fsr, prec, pe, ps1, pb1, c10::nullopt, act1);
+        at::Tensor d = qconv2d_packed(h, wd, ws_d, c10::nullopt, {s.S, s.S}, {1, 1}, {1, 1}, s.Ch, bits, mode, fsr,
+                                      prec, pd, ps2, pb2, c10::nullopt, act2);
+        return qconv2d_packed(d, wp, ws_p, c10::nullopt, {1, 1}, {0, 0}, {1, 1}, 1, bits, mode, fsr, prec, pp, ps3,
+                              pb3, residual, act3);
+    }
+    const at::Tensor x = x_.contiguous();
+    const std::vector<int64_t> yshape{s.N, s.Cout, s.Ho, s.Wo};
+    std::array<c10::optional<at::Tensor>, 6> vc;
+    const c10::optional<at::Tensor>* vs[6] = {&ps1, &pb1, &ps2, &pb2, &ps3, &pb3};
+    const char* names[6] = {"ps1", "pb1", "ps2", "pb2", "ps3", "pb3"};
+    for (int i = 0; i < 6; ++i) {
+        check_vec(*vs[i], x, i < 4 ? s.Ch : s.Cout, names[i]);
+        if (vs[i]->has_value()) vc[i] = (*vs[i])->contiguous();
+    }
+    c10::optional<at::Tensor> res;
+    if (residual.has_value()) {
+        check_hip_f32(*residual, "residual");
+        TORCH_CHECK(residual->device() == x.device() && residual->sizes() == at::IntArrayRef(yshape),
+                    "po2q: residual shape ", residual->sizes(), " does not match the output ", at::IntArrayRef(yshape));
+        res = residual->contiguous();
+    }
+    for (const at::Tensor* t : {&ws_d, &ws_p})
+        TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kByte && t->is_contiguous() && t->device() == x.device(),
+                    "po2q: inverted residual: workspaces must be contiguous uint8 tensors on the input's device");
+    if (ws_e.has_value())  // NOLINT
+        TORCH_CHECK(ws_e->is_cuda() && ws_e->scalar_type() == at::kByte && ws_e->is_contiguous() &&
+                        ws_e->device() == x.device(),
+                    "po2q: inverted residual: workspaces must be contiguous uint8 tensors on the input's device");
+    at::Tensor y = at::empty(yshape, x.options());
+    const int st = po2q_qconv2d_ir_f32(
+        x.data_ptr<float>(), y.data_ptr<float>(), ee ? ee->plan : nullptr, ws_e.has_value() ? ws_e->data_ptr() : nullptr,
+        ws_e.has_value() ? (size_t)ws_e->numel() : 0, ed->plan, ws_d.data_ptr(), (size_t)ws_d.numel(), ep->plan,
+        ws_p.data_ptr(), (size_t)ws_p.numel(), opt_ptr(vc[0]), opt_ptr(vc[1]), (int)act1, opt_ptr(vc[2]),
+        opt_ptr(vc[3]), (int)act2, opt_ptr(vc[4]), opt_ptr(vc[5]), opt_ptr(res), (int)act3, stream_of(x));
+    TORCH_CHECK(st == 0, last_error());
+    return y;
+}
+
+at::Tensor qconv2d_ir_meta(const at::Tensor& x, const c10::optional<at::Tensor>& we, const at::Tensor& wd,
+                           const at::Tensor& wp, const c10::optional<at::Tensor>&, const at::Tensor&, const at::Tensor&,
+                           int64_t stride, int64_t, int64_t, int64_t, int64_t, const c10::optional<at::Tensor>&,
+                           const c10::optional<at::Tensor>&, int64_t, const c10::optional<at::Tensor>&,
+                           const c10::optional<at::Tensor>&, int64_t, const c10::optional<at::Tensor>&,
+                           const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, int64_t,
+                           at::IntArrayRef) {
+    const IrShape s = ir_shape(x, we, wd, wp, stride);
+    return at::empty({s.N, s.Cout, s.Ho, s.Wo}, x.options());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(po2q, m) {
@@ -667,6 +786,10 @@ TORCH_LIBRARY(po2q, m) {
     m.def("qconv2d_packed(Tensor x, Tensor w, Tensor workspace, Tensor? bias, int[2] stride, int[2] padding, "
           "int[2] dilation, int groups, int bits, int mode, int fsr=1, int precision=0, int plan=-1, "
           "Tensor? post_scale=None, Tensor? post_shift=None, Tensor? residual=None, int act=0) -> Tensor");
+    m.def("qconv2d_ir(Tensor x, Tensor? we, Tensor wd, Tensor wp, Tensor? ws_e, Tensor ws_d, Tensor ws_p, "
+          "int stride, int bits, int mode, int fsr=1, int precision=0, Tensor? ps1=None, Tensor? pb1=None, "
+          "int act1=0, Tensor? ps2=None, Tensor? pb2=None, int act2=0, Tensor? ps3=None, Tensor? pb3=None, "
+          "Tensor? residual=None, int act3=0, int[] plans=[]) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches HIP tensors under CUDA)
@@ -681,6 +804,7 @@ TORCH_LIBRARY_IMPL(po2q, CUDA, m) {  // the HIP device (PyTorch-ROCm dispatches 
     m.impl("qconv2d_chain", &qconv2d_chain);
     m.impl("qconv2d_pack_batch", &qconv2d_pack_batch);
     m.impl("qconv2d_packed", &qconv2d_packed);
+    m.impl("qconv2d_ir", &qconv2d_ir);
 }
 
 TORCH_LIBRARY_IMPL(po2q, Meta, m) {
@@ -695,4 +819,5 @@ TORCH_LIBRARY_IMPL(po2q, Meta, m) {
     m.impl("qconv2d_chain", &qconv2d_chain_meta);
     m.impl("qconv2d_pack_batch", &qconv2d_pack_batch_meta);
     m.impl("qconv2d_packed", &qconv2d_packed_meta);
+    m.impl("qconv2d_ir", &qconv2d_ir_meta);
 }

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from .quantized_conv import (QuantizedConv2d, batched_packs, can_fuse, fusable_sequence, run_fused_sequence,
-                             run_sequence)
+                             run_inverted_residual, run_sequence)
 
 
 def quantized_conv_1x1_bn(inp, oup, quantize_fn=None, bits=4):
@@ -128,7 +128,7 @@ class MV2Block(nn.Module):
 
     def forward(self, x):
         if can_fuse(*self.conv) and fusable_sequence(self.conv):
-            return run_fused_sequence(self.conv, x, residual=x if self.use_res_connect else None)
+            return run_inverted_residual(self.conv, x, residual=x if self.use_res_connect else None)
         y = self.conv(x)
         return y + x if self.use_res_connect else y
 

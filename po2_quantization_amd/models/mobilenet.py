@@ -23,7 +23,7 @@ from typing import Any, Callable, Optional
 import torch.nn as nn
 
 from .quantized_conv import (QuantizedConv2d, batched_packs, can_fuse, fusable_sequence, run_fused_sequence,
-                             run_sequence)
+                             run_inverted_residual, run_sequence)
 
 # (expand ratio t, output channels c, repeats n, first stride s) -- mobilenet.py:153-161
 MOBILENET_V2_SETTINGS = ((1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2),
@@ -72,7 +72,7 @@ class InvertedResidual(nn.Module):
 
     def forward(self, x):
         if can_fuse(*self.conv) and fusable_sequence(self.conv):
-            return run_fused_sequence(self.conv, x, residual=x if self.identity else None)
+            return run_inverted_residual(self.conv, x, residual=x if self.identity else None)
         y = self.conv(x)
         return x + y if self.identity else y
 

@@ -173,15 +173,17 @@ class _ForwardPacks:
     def __init__(self, layers):
         self.recording = [] if layers is None else None
         self.ws = {}
+        self.fixed = {}  # id(conv) -> plan index while recording an inverted-residual block's layers
         if layers is None:
             return
         groups = {}
-        for m, g, conf in layers:
-            groups.setdefault(conf, []).append((m, g))
+        for m, g, conf, plan in layers:
+            groups.setdefault(conf, []).append((m, g, plan))
         for (bits, mode, prec), items in groups.items():
-            ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g in items], bits, mode, 1, prec)
-            for (m, g), w in zip(items, ws):
-                self.ws[id(m)] = (g, m.weight, w)
+            ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g, _ in items], bits, mode, 1, prec,
+                                 plans=[pl for _, _, pl in items])
+            for (m, g, pl), w in zip(items, ws):
+                self.ws[id(m)] = (g, m.weight, w, pl)
 
 
 @contextlib.contextmanager
@@ -192,7 +194,7 @@ def batched_packs(model, x):
             or not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32)):
         yield
         return
-    key = (tuple(x.shape), x.device, INFERENCE_FUSION)
+    key = (tuple(x.shape), x.device, INFERENCE_FUSION, IR_FUSION)
     rec = model.__dict__.setdefault("_po2q_packs", {})
     sess = _ForwardPacks(rec.get(key))
     _packs = sess
@@ -274,13 +276,13 @@ class QuantizedConv2d(nn.Conv2d):
         if sess is not None and mode != "none" and input.dim() == 4:
             g = (tuple(input.shape), tuple(self.stride), tuple(self._padding(input)), tuple(self.dilation), self.groups)
             if sess.recording is not None:
-                sess.recording.append((self, g, (self.bits, mode, self.precision)))
+                sess.recording.append((self, g, (self.bits, mode, self.precision), sess.fixed.get(id(self))))
             else:
                 hit = sess.ws.get(id(self))
                 if hit is not None and hit[0] == g and hit[1] is weight and hit[2].numel() > 0:
                     return _lib.qconv2d_packed(input, weight, hit[2], self.bias, g[1], g[2], g[3], g[4], self.bits,
                                                mode, 1, self.precision, post_scale=ps, post_shift=pb,
-                                               residual=residual, act=act or "none")
+                                               residual=residual, act=act or "none", plan=hit[3])
         return _lib.qconv2d_fused(input, weight, self.bias, self.stride, self._padding(input), self.dilation,
                                   self.groups, self.bits, mode, 1, self.precision, post_scale=ps, post_shift=pb,
                                   residual=residual, act=act or "none")
@@ -351,6 +353,81 @@ def run_fused_sequence(seq, x, residual=None):
         else:
             x = plain_conv_fused(conv, x, bn=bn, act=act, residual=res)
     return x
+
+
+# Whole inverted-residual blocks (mobilenet.py:53-134, mobile_vit.py:131-239) as ONE launch
+# (torch.ops.po2q.qconv2d_ir: expand -> depthwise -> project with the hidden activations on
+# chip) inside a batched_packs forward, from the three layers' batched packs.  False: the three
+# fused layer calls (A/B runs).
+IR_FUSION = True
+
+
+def _ir_spec(seq):
+    """(expand | None, depthwise, project) (conv, bn, act) groups when seq is an inverted-residual
+    conv block the fused kernel reproduces: bias-free QuantizedConv2d layers with one native
+    quantizer / bits / precision, 1x1 expand, 3x3 pad-1 depthwise (stride 1 or 2), 1x1 project."""
+    spec = seq.__dict__.get("_po2q_ir")
+    if spec is not None:
+        return spec or None
+    groups, mods, i = [], list(seq), 0
+    while i < len(mods):
+        conv, bn, act = mods[i], None, None
+        i += 1
+        if i < len(mods) and isinstance(mods[i], nn.modules.batchnorm._BatchNorm):
+            bn, i = mods[i], i + 1
+        if i < len(mods) and act_name(mods[i]) is not None:
+            act, i = act_name(mods[i]), i + 1
+        groups.append((conv, bn, act))
+    ok = len(groups) in (2, 3) and all(isinstance(g[0], QuantizedConv2d) for g in groups)
+    if ok:
+        convs = [g[0] for g in groups]
+        conf = {(c.bits, c.quantize_fn, c.precision) for c in convs}
+        ok = (len(conf) == 1 and NATIVE_MODES.get(convs[0].quantize_fn) is not None
+              and all(c.bias is None and c.padding_mode == "zeros" and not isinstance(c.padding, str)
+                      and tuple(c.dilation) == (1, 1) for c in convs))
+    if ok:
+        d, p = convs[-2], convs[-1]
+        pw = lambda c: tuple(c.kernel_size) == (1, 1) and tuple(c.stride) == (1, 1) and tuple(c.padding) == (0, 0) \
+            and c.groups == 1
+        ok = (tuple(d.kernel_size) == (3, 3) and tuple(d.padding) == (1, 1) and d.stride[0] == d.stride[1]
+              and d.stride[0] in (1, 2) and d.groups == d.in_channels == d.out_channels and pw(p)
+              and (len(convs) == 2 or pw(convs[0])))
+    spec = (([None] if len(groups) == 2 else []) + groups) if ok else ()
+    seq.__dict__["_po2q_ir"] = spec
+    return spec or None
+
+
+def run_inverted_residual(seq, x, residual=None):
+    """run_fused_sequence(seq, x, residual) for an inverted-residual conv block: ONE qconv2d_ir launch
+    when a batched_packs forward holds the three layers' packs, else the per-layer fused calls
+    (which record the layers for the next forward's packs)."""
+    sess = _packs
+    spec = _ir_spec(seq) if IR_FUSION and sess is not None else None
+    if spec is not None and sess.recording is not None:
+        # record the block's layers with their heuristic plans (candidate 0: the pointwise and
+        # depthwise kernels whose packs the block kernel reads), whatever the autotuner picked
+        for g in spec:
+            if g is not None:
+                sess.fixed[id(g[0])] = 0
+        spec = None
+    if spec is not None and x.dim() == 4:
+        hits = []
+        for g in spec:
+            hit = sess.ws.get(id(g[0])) if g is not None else None
+            if g is not None and (hit is None or hit[1] is not g[0].weight or hit[2].numel() == 0 or hit[3] != 0):
+                break
+            hits.append(hit)
+        else:
+            e, d, p = spec
+            if (hits[0] if e is not None else hits[1])[0][0] == tuple(x.shape):
+                f = [fold_bn(g[1]) if g is not None and g[1] is not None else (None, None) for g in spec]
+                conv = d[0]
+                return _lib.qconv2d_ir(x, e[0].weight if e else None, d[0].weight, p[0].weight,
+                                       hits[0][2] if e else None, hits[1][2], hits[2][2], conv.stride[0], conv.bits,
+                                       NATIVE_MODES[conv.quantize_fn], 1, conv.precision,
+                                       f[0][0], f[0][1], e[2] if e else None, f[1][0], f[1][1], d[2], f[2][0],
+                                       f[2][1], residual, p[2])
+    return run_fused_sequence(seq, x, residual=residual)
 
 
 def run_sequence(seq, x):

@@ -75,3 +75,43 @@ def test_chain_list_lengths_checked():
     for kw in ({"acts": ["relu"] * 2}, {"res_from": [-1, 0]}, {"biases": [None] * 4}, {"post_scales": []}):
         with pytest.raises(_lib.Po2qError, match="one entry per weight"):
             _lib.qconv2d_chain(x, w, **kw)
+
+
+@pytest.mark.parametrize("Cin,Ch,Cout,H,stride,expand", [(16, 96, 24, 16, 2, True), (32, 32, 16, 16, 1, False),
+                                                          (160, 960, 320, 1, 1, True), (12, 80, 20, 9, 2, True)])
+def test_ir_op_meta_shape(Cin, Ch, Cout, H, stride, expand):
+    """qconv2d_ir (a whole inverted-residual block in one launch): the project conv's output shape
+    of the depthwise conv's output, as the three F.conv2d calls give it."""
+    O = _lib.ops()
+    x = torch.empty(3, Cin, H, H, device="meta")
+    we = torch.empty(Ch, Cin, 1, 1, device="meta") if expand else None
+    wd = torch.empty(Ch, 1, 3, 3, device="meta")
+    wp = torch.empty(Cout, Ch, 1, 1, device="meta")
+    ws = torch.empty(0, dtype=torch.uint8, device="meta")
+    y = O.qconv2d_ir(x, we, wd, wp, ws if expand else None, ws, ws, stride, 4, 1)
+    F = torch.nn.functional
+    h = F.conv2d(x, we) if expand else x
+    want = F.conv2d(F.conv2d(h, wd, None, stride, 1, 1, Ch), wp).shape
+    assert y.shape == want
+    with pytest.raises(RuntimeError, match="project weight"):
+        O.qconv2d_ir(x, we, wd, torch.empty(Cout, Ch + 1, 1, 1, device="meta"), ws if expand else None, ws, ws,
+                     stride, 4, 1)
+
+
+def test_ir_block_detection():
+    """The models' inverted-residual conv blocks are recognised for the fused launch; a quantizer-free
+    block (mode none: nothing to pack) and a 3x3-conv block are not."""
+    from po2_quantization_amd.models import quantized_conv as qc
+    from po2_quantization_amd.models.mobilenet import InvertedResidual
+    from po2_quantization_amd.utils.quantizers import quantizer_dict
+
+    q = quantizer_dict["po2"]
+    blk = InvertedResidual(24, 24, 1, 6, quantize_fn=q)
+    e, d, p = qc._ir_spec(blk.conv)
+    assert e[2] == "relu6" and d[2] == "relu6" and p[2] is None and d[0].groups == 144
+    blk1 = InvertedResidual(32, 16, 1, 1, quantize_fn=q)
+    e, d, p = qc._ir_spec(blk1.conv)
+    assert e is None and d[0].groups == 32
+    assert qc._ir_spec(InvertedResidual(24, 24, 1, 6, quantize_fn=None).conv) is None
+    from po2_quantization_amd.models.mobilenet import quantized_conv_3x3_bn
+    assert qc._ir_spec(quantized_conv_3x3_bn(16, 16, 1, quantize_fn=q)) is None

@@ -11,5 +11,4 @@ run() {  # name timeout cmd...
 }
 run t3_tests 900 python -u -m pytest tests/test_gpu_packs.py tests/test_gpu_split.py tests/test_gpu_chain.py tests/test_gpu_models.py tests/test_qat.py -m gpu -x -q --timeout 300 --timeout-method thread
 run t3_pairmw 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -q --timeout 300 --timeout-method thread -k "memory_wave or full_size or vs_oracle"
-run pair_stamps 300 python -u tools/pair_stamps.py
 run pair_mw 300 python -u tools/pair_mw_bench.py

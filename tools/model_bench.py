@@ -46,7 +46,10 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="also time the fused forward replayed from a HIP graph (small images: launch-bound)")
     ap.add_argument("--only-fused", action="store_true")
+    ap.add_argument("--no-ir", action="store_true",
+                    help="inverted-residual blocks as three fused layer calls instead of one block launch")
     args = ap.parse_args()
+    quantized_conv.IR_FUSION = not args.no_ir
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
     m = get_model(args.model, args.classes, quantizer_dict[args.quantizer], args.bits,
@@ -54,7 +57,7 @@ def main():
     x = torch.randn(args.batch, 3, args.image, args.image, device=dev)
     _lib.benchmark = True  # autotune every conv shape once (cudnn.benchmark counterpart)
     res = {"model": args.model, "image": args.image, "batch": args.batch, "quantizer": args.quantizer,
-           "bits": args.bits}
+           "bits": args.bits, "ir_fusion": quantized_conv.IR_FUSION}
     with torch.no_grad():
         for name, fuse in (("fused", True), ("unfused", False)):
             if args.only_fused and not fuse:
