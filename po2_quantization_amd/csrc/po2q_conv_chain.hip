@@ -123,7 +123,10 @@ __device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mi
 // lanes that will add it: every layer maps (wave, lane) to the same (pixel, channels).
 // FULL: every wave owns exactly MG whole groups (H * W a multiple of 16 * waves per tile * MG):
 // no per-group bounds checks (the CIFAR stages).
-template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = false>
+// DB (C = 32 / 64): two plane sets, layer l reads set l & 1 and writes set (l + 1) & 1, so the
+// barrier between a layer's MFMA phase and its epilogue goes: a wave's epilogue runs under the
+// other waves' MFMAs, one barrier per layer.
+template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = false, bool DB = false>
 __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __restrict__ x, float* __restrict__ y,
                                                                ChainArgs a) {
     constexpr int KS = C == 16 ? 2 : 3 * (C / 32);  // k-steps per tap row
@@ -172,6 +175,10 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         }
     }
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.PL + a.ZO) = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (DB) {  // the second set's zero halo (and zero slot): the whole set zeroed once
+        for (int i = tid; i < 3 * a.PL / 16; i += kChainThreads)
+            *reinterpret_cast<uint4*>(lds + 3 * a.PL + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+    }
     // the held residual: x itself when a later layer adds it
     float rres[MG][4];
 #pragma unroll
@@ -304,6 +311,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
 
     for (int l = 0; l < a.L; ++l) {
         const ChainLayer& ly = a.layer[l];
+        const int rd = DB ? (l & 1) * 3 * a.PL : 0, wr = DB ? ((l + 1) & 1) * 3 * a.PL : 0;
         // this layer's epilogue constants: loaded now, consumed after the MFMA phase
         const float scale = *ly.scale;
         float cbk[4], ceps[4], cepb[4];
@@ -333,7 +341,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
                     ring[st % (PD + 1)][pl] =
-                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + pl * a.PL + ad));
+                        __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + rd + pl * a.PL + ad));
             }
         };
         auto step = [&](auto ST_) __attribute__((always_inline)) {
@@ -356,9 +364,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         const int act = ly.act, res_add = ly.res_add, keep = ly.keep;
         load_bw(a.layer[last ? l : l + 1]);
         // every read of this layer's input planes has retired.  A bare s_barrier, not
-        // __syncthreads: its release fence would wait for the prefetches just issued (vmcnt(0))
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        // __syncthreads: its release fence would wait for the prefetches just issued (vmcnt(0)).
+        // DB: the epilogue writes the other set, nothing to wait for
+        if constexpr (!DB) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
 
         // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p
 #pragma unroll
@@ -382,9 +393,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 const int ad = ch_addr<C, W8, S16>((oy + 1) * PW + ox + 1, ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
                 uint2 hi, mid, lo;
                 split4(v, hi, mid, lo);
-                *reinterpret_cast<uint2*>(lds + ad) = hi;
-                *reinterpret_cast<uint2*>(lds + a.PL + ad) = mid;
-                *reinterpret_cast<uint2*>(lds + 2 * a.PL + ad) = lo;
+                *reinterpret_cast<uint2*>(lds + wr + ad) = hi;
+                *reinterpret_cast<uint2*>(lds + wr + a.PL + ad) = mid;
+                *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
             }
         }
         // the next layer's input planes are complete (the block's own LDS writes: lgkmcnt)
@@ -555,14 +566,16 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
         ly.res_add = (res_from && res_from[l] >= 0) ? 1 : 0;
         ly.keep = used[l + 1];
     }
-    const size_t lds = 3 * (size_t)a.PL;
+    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes
+    // swizzled, bit 2 double-buffered planes (C = 32 / 64, when two sets fit)
+    const char* venv = getenv("PO2Q_CHAIN_VARIANT");
+    const int variant = venv ? atoi(venv) : 0;
+    const bool db = (variant & 4) && C != 16 && 6 * (size_t)a.PL <= kChainLdsMax;
+    const size_t lds = (db ? 6 : 3) * (size_t)a.PL;
     const dim3 grid((unsigned)N), block(kChainThreads);
     const int mg = chain_mg(C, H, W);
     const bool w8 = C == 64 && W == 8;
     const int64_t wpt = (kChainThreads / 64) / (C / 16);
-    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes swizzled
-    const char* venv = getenv("PO2Q_CHAIN_VARIANT");
-    const int variant = venv ? atoi(venv) : 0;
     const bool full = !(variant & 1) && (H * W) % 16 == 0 && (H * W / 16) % wpt == 0;
     // the exact-fit forms (FULL) for the CIFAR stages, the checked forms for everything else
 #define PO2Q_CH(c, m, w)                                                                               \
@@ -572,6 +585,11 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
                 hipLaunchKernelGGL((conv_chain<c, m, w, true, true>), grid, block, lds, s, x, y, a);   \
             else                                                                                       \
                 hipLaunchKernelGGL((conv_chain<c, m, w, false, true>), grid, block, lds, s, x, y, a);  \
+        } else if (c != 16 && db) {                                                                    \
+            if (full && mg == m)                                                                       \
+                hipLaunchKernelGGL((conv_chain<c, m, w, true, false, true>), grid, block, lds, s, x, y, a); \
+            else                                                                                       \
+                hipLaunchKernelGGL((conv_chain<c, m, w, false, false, true>), grid, block, lds, s, x, y, a); \
         } else if (full && mg == m) {                                                                  \
             hipLaunchKernelGGL((conv_chain<c, m, w, true>), grid, block, lds, s, x, y, a);            \
         } else {                                                                                       \

@@ -15,3 +15,5 @@ run mb_ir 300 python tools/model_bench.py --model mobilenet --image 32 --classes
 run mb_noir 300 python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --only-fused --graph --no-ir
 run t5_pairmw 600 python -u -m pytest tests/test_gpu_pair.py -m gpu -x -q --timeout 300 --timeout-method thread -k "memory_wave or full_size or vs_oracle"
 run pair_mw 300 python -u tools/pair_mw_bench.py
+run t5_chain 400 python -u -m pytest tests/test_gpu_chain.py -m gpu -x -q --timeout 300 --timeout-method thread
+run chain_ab 300 python -u tools/chain_ab.py
