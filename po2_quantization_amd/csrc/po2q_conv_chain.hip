@@ -567,10 +567,12 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
         ly.keep = used[l + 1];
     }
     // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes
-    // swizzled, bit 2 double-buffered planes (C = 32 / 64, when two sets fit)
+    // swizzled, bit 3 one plane set.  Default: double-buffered planes for C = 32 / 64 (two sets
+    // fit): 0.0849 vs 0.0861 ms at 32 x 16^2 and 0.0782 vs 0.0795 at 64 x 8^2, 17 layers bs 256,
+    // 5 of 5 interleaved rounds (profiles/r04_chain_ab_db.jsonl)
     const char* venv = getenv("PO2Q_CHAIN_VARIANT");
     const int variant = venv ? atoi(venv) : 0;
-    const bool db = (variant & 4) && C != 16 && 6 * (size_t)a.PL <= kChainLdsMax;
+    const bool db = !(variant & 8) && C != 16 && 6 * (size_t)a.PL <= kChainLdsMax;
     const size_t lds = (db ? 6 : 3) * (size_t)a.PL;
     const dim3 grid((unsigned)N), block(kChainThreads);
     const int mg = chain_mg(C, H, W);

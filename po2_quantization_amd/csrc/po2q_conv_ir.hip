@@ -10,17 +10,22 @@
 // of work, so the layer-by-layer forward is ~50 latency-bound launches whose HBM traffic is
 // dominated by the 6x-wide hidden tensors (written by the expand, read + written by the depthwise,
 // read by the project).  Here a block owns a band of R output rows of G images (G > 1 only when
-// one image is one band) and walks the hidden channels in chunks of CHK (a multiple of 32):
+// one image is one band) and walks the hidden channels in chunks of CHK = 32 KC:
 //   prologue   the band's input rows (+ the depthwise halo) of x -> LDS fp32 [pixel][Cin + pad];
-//   per chunk  expand: (16-pixel group, pair of 16-channel tiles) units on v_mfma_f32_16x16x32_bf16
-//              (A = the exact hi / mid / lo bf16 split of x, B = the expand layer's pointwise
-//              pack), bn1 + act1 -> hidden fp32 [channel][pixel];  barrier;
+//   per chunk  expand: each wave owns one pair of 16-channel tiles and walks the 16-pixel groups on
+//              v_mfma_f32_16x16x32_bf16 (A = the exact hi / mid / lo bf16 split of x, B = the expand
+//              layer's pointwise pack), bn1 + act1 -> hidden fp32 [channel][pixel];  barrier;
 //              depthwise 3x3: fp32 FMAs in conv_dw3's tap order (the quantized depthwise weight
 //              is exact fp32), bn2 + act2, exact split -> bf16 planes [output pixel][CHK];
 //              barrier;
-//              project: every wave accumulates its (output-pixel group, output-channel tile)
-//              units over the chunk's k-steps (B = the project layer's pointwise pack);
+//              project: every wave accumulates its (output-pixel group, output-channel tile) units
+//              over the chunk's KC k-steps (B = the project layer's pointwise pack);
 //   epilogue   bn3 (+ the residual x) + act3 -> y.
+// Latency, not arithmetic, bounds a block at these sizes (a few hundred MFMAs per chunk), so no
+// weight load sits on the critical path: each wave's expand and project B fragments for the next
+// chunk are loaded into registers right after it used this chunk's (they land under the other
+// phases), and the chunk's depthwise weights + BN vectors are loaded before the expand and parked
+// in LDS after it.
 // Weights come from the three layers' own packs (qconv2d_pack_batch: the pointwise [ks][nt][lane]
 // bf16 fragments + scale multiplier, the depthwise plain quantized fp32 copy), so every weight is
 // still quantized in every forward.  Arithmetic per layer is the layer kernels' own (conv_pw's
@@ -40,15 +45,17 @@ namespace po2q {
 namespace {
 constexpr int kIrThreads = 512;  // 8 waves
 constexpr int kIrWaves = kIrThreads / 64;
-constexpr int kIrUnits = 8;  // project units (output-pixel group x output-channel tile) per wave
+constexpr int kIrKse = 5;     // expand k-steps held in registers: Cin <= 160
+constexpr int kIrCw = 12;     // staged depthwise parameters per hidden channel: 9 taps, bn scale, shift, pad
 constexpr size_t kIrLds = 150 * 1024;
+// project units one wave holds B fragments for, by k-steps per chunk (<= 16 fragments = 64 VGPRs)
+constexpr int ir_umax(int kc) { return kc >= 8 ? 2 : (kc >= 4 ? 4 : 8); }
 }  // namespace
 
 struct IrArgs {
     int N, Cin, H, W, Ch, Cout, S, Ho, Wo;
     int G, R, RI, nbands;  // images per block, output / input rows per band, bands per image
-    int CHK;               // hidden channels per chunk (multiple of 32)
-    int KSe, NTe, NTp;     // expand k-steps (32 ch), expand / project 16-channel output tiles
+    int KSe, NTe, KSp, NTp;  // expand / project k-steps (32 ch) and 16-channel output tiles
     int xs;                // x row stride in LDS (floats): 32 KSe + 4
     int P, PG, Po, HP;     // input pixels, their 16-groups, output pixels (x16) of a block; hidden row stride
     const uint4* we;       // expand pack (NULL: h = x)
@@ -59,11 +66,15 @@ struct IrArgs {
     const float *ps1, *pb1, *ps2, *pb2, *ps3, *pb3;
     int act1, act2, act3;
     const float* res;      // residual [N, Cout, Ho, Wo] or NULL
-    int off_hid, off_dpl;  // LDS byte offsets
+    int off_hid, off_dpl, off_cw;  // LDS byte offsets
 };
 
-// LDS: x [16 PG][xs] fp32 (expand only) | hidden chunk [CHK][HP] fp32 | d planes 3 x [Po][CHK] bf16
+// LDS: x [16 PG][xs] fp32 (expand only) | hidden chunk [CHK][HP] fp32 | d planes 3 x [Po][CHK] bf16 |
+// the chunk's depthwise parameters [CHK][12] fp32.  KC: project k-steps per chunk (CHK = 32 KC).
+template <int KC>
 __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ x, float* __restrict__ y, IrArgs a) {
+    constexpr int CHK = 32 * KC;
+    constexpr int UMAX = ir_umax(KC);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -76,8 +87,45 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
     float* xl = reinterpret_cast<float*>(lds);
     float* hid = reinterpret_cast<float*>(lds + a.off_hid);
     unsigned char* dpl = lds + a.off_dpl;
-    const int drow = a.CHK * 2;        // bytes per output pixel of a d plane
-    const int dplane = a.Po * drow;    // bytes per d plane
+    float* cw = reinterpret_cast<float*>(lds + a.off_cw);
+    constexpr int drow = CHK * 2;     // bytes per output pixel of a d plane
+    const int dplane = a.Po * drow;   // bytes per d plane
+    const int nunits = a.Po / 16 * a.NTp;
+    constexpr uint4 z4 = {0u, 0u, 0u, 0u};
+
+    // ---- register-held B fragments: this wave's expand tile pair and its project units
+    const int tp = wave % KC;  // the expand tile pair this wave owns in every chunk
+    uint4 bwe[kIrKse][2];
+    float e1s[2], e1b[2];
+    auto load_bwe = [&](int c0n) __attribute__((always_inline)) {
+        const int ntile = min(CHK, a.Ch - c0n) / 16;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const bool tok = 2 * tp + t < ntile;  // wave-uniform
+            const int tile = c0n / 16 + 2 * tp + t;
+#pragma unroll
+            for (int ks = 0; ks < kIrKse; ++ks)
+                bwe[ks][t] = (tok && ks < a.KSe) ? a.we[((int64_t)ks * a.NTe + tile) * 64 + lane] : z4;
+            const int h = 16 * tile + pl;
+            e1s[t] = (tok && a.ps1) ? a.ps1[h] : 1.0f;
+            e1b[t] = (tok && a.pb1) ? a.pb1[h] : 0.0f;
+        }
+    };
+    uint4 bwp[UMAX][KC];
+    auto load_bwp = [&](int c0n) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) {
+            const int u = wave + kIrWaves * i;
+            const int ot = u % a.NTp;
+#pragma unroll
+            for (int k2 = 0; k2 < KC; ++k2) {
+                const int ks = c0n / 32 + k2;
+                bwp[i][k2] = (u < nunits && ks < a.KSp) ? a.wp[((int64_t)ks * a.NTp + ot) * 64 + lane] : z4;
+            }
+        }
+    };
+    if (expand) load_bwe(0);
+    load_bwp(0);
 
     // the band's input pixel px (image, row iy0 + ry, column) of channel c; 0 outside
     auto x_at = [&](int c, int px) -> float {
@@ -87,7 +135,6 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
         if (img >= a.G || n0 + img >= a.N || iy > iy1 || c >= a.Cin) return 0.0f;
         return x[(((int64_t)(n0 + img) * a.Cin + c) * a.H + iy) * a.W + ix];
     };
-
     if (expand) {
         const int cinp = 32 * a.KSe, P16 = 16 * a.PG;
         for (int u = tid; u < P16 * cinp; u += kIrThreads) {
@@ -98,69 +145,91 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
     const float se = expand ? *a.we_scale : 1.0f;
     const float sp = *a.wp_scale;
 
-    const int nunits = a.Po / 16 * a.NTp;
-    floatx4 acc[kIrUnits];
+    floatx4 acc[UMAX];
 #pragma unroll
-    for (int i = 0; i < kIrUnits; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < UMAX; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    for (int c0 = 0; c0 < a.Ch; c0 += a.CHK) {
-        const int CH = min(a.CHK, a.Ch - c0);  // a multiple of 16
-        __syncthreads();  // x staged / the previous chunk's depthwise reads of hid retired
+    constexpr int CWPT = (CHK * 11 + kIrThreads - 1) / kIrThreads;  // staged parameters per thread
+    for (int c0 = 0; c0 < a.Ch; c0 += CHK) {
+        const int CH = min(CHK, a.Ch - c0);  // a multiple of 16
+        // the chunk's depthwise taps and BN vectors: loaded now, parked in LDS after the expand
+        float cwv[CWPT];
+#pragma unroll
+        for (int j = 0; j < CWPT; ++j) {
+            const int idx = tid + kIrThreads * j;
+            const int hc = idx / 11, k = idx - hc * 11;
+            float v = 0.0f;
+            if (hc < CH) {
+                const int h = c0 + hc;
+                v = k < 9 ? a.wd[h * 9 + k] : (k == 9 ? (a.ps2 ? a.ps2[h] : 1.0f) : (a.pb2 ? a.pb2[h] : 0.0f));
+            }
+            cwv[j] = v;
+        }
+        __syncthreads();  // x staged / the previous chunk's depthwise reads of hid and cw retired
         // ---- expand (or copy x) -> hid [CH][HP] fp32
         if (expand) {
-            const int ntile = CH / 16, npair = (ntile + 1) / 2;
-            for (int u = wave; u < a.PG * npair; u += kIrWaves) {
-                const int pg = u / npair, tp = u - pg * npair;
-                const int t0 = 2 * tp, nt = min(2, ntile - t0);
-                floatx4 c[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
-                const float* xr = xl + (16 * pg + pl) * a.xs + 8 * g;
-                for (int ks = 0; ks < a.KSe; ++ks) {
-                    const floatx4 v0 = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
-                    const floatx4 v1 = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
-                    const uint32_t b[8] = {__float_as_uint(v0[0]), __float_as_uint(v0[1]), __float_as_uint(v0[2]),
-                                           __float_as_uint(v0[3]), __float_as_uint(v1[0]), __float_as_uint(v1[1]),
-                                           __float_as_uint(v1[2]), __float_as_uint(v1[3])};
-                    uint4 hi, mid, lo;
-                    split3(b, hi, mid, lo);
-                    const bf16x8 ah = __builtin_bit_cast(bf16x8, hi), am = __builtin_bit_cast(bf16x8, mid),
-                                 al = __builtin_bit_cast(bf16x8, lo);
+            const int ntile = CH / 16, t0 = 2 * tp, nt = min(2, ntile - t0);
+            if (nt > 0) {  // wave-uniform
+                for (int pg = wave / KC; pg < a.PG; pg += kIrWaves / KC) {
+                    floatx4 c[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+                    const float* xr = xl + (16 * pg + pl) * a.xs + 8 * g;
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        if (t < nt) {  // wave-uniform
-                            const int tile = c0 / 16 + t0 + t;
-                            const bf16x8 bw = __builtin_bit_cast(bf16x8, a.we[((int64_t)ks * a.NTe + tile) * 64 + lane]);
-                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, c[t], 0, 0, 0);
-                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, c[t], 0, 0, 0);
-                            c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, c[t], 0, 0, 0);
+                    for (int ks = 0; ks < kIrKse; ++ks) {
+                        if (ks >= a.KSe) break;
+                        const floatx4 v0 = *reinterpret_cast<const floatx4*>(xr + 32 * ks);
+                        const floatx4 v1 = *reinterpret_cast<const floatx4*>(xr + 32 * ks + 4);
+                        const uint32_t b[8] = {__float_as_uint(v0[0]), __float_as_uint(v0[1]),
+                                               __float_as_uint(v0[2]), __float_as_uint(v0[3]),
+                                               __float_as_uint(v1[0]), __float_as_uint(v1[1]),
+                                               __float_as_uint(v1[2]), __float_as_uint(v1[3])};
+                        uint4 hi, mid, lo;
+                        split3(b, hi, mid, lo);
+                        const bf16x8 ah = __builtin_bit_cast(bf16x8, hi), am = __builtin_bit_cast(bf16x8, mid),
+                                     al = __builtin_bit_cast(bf16x8, lo);
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) {
+                            if (t < nt) {  // wave-uniform
+                                const bf16x8 bw = __builtin_bit_cast(bf16x8, bwe[ks][t]);
+                                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, c[t], 0, 0, 0);
+                                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, c[t], 0, 0, 0);
+                                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, c[t], 0, 0, 0);
+                            }
                         }
                     }
-                }
-                // lane: hidden channel c0 + 16 (t0 + t) + pl, pixels 16 pg + 4 g .. + 3 (conv_pw's epilogue)
+                    // lane: hidden channel c0 + 16 (t0 + t) + pl, pixels 16 pg + 4 g .. + 3 (conv_pw's epilogue)
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    if (t >= nt) break;
-                    const int hc = 16 * (t0 + t) + pl, h = c0 + hc;
-                    const float s1 = a.ps1 ? a.ps1[h] : 1.0f, b1 = a.pb1 ? a.pb1[h] : 0.0f;
-                    floatx4 v;
+                    for (int t = 0; t < 2; ++t) {
+                        if (t >= nt) break;
+                        const int hc = 16 * (t0 + t) + pl;
+                        floatx4 v;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float q = c[t][e] * se + 0.0f;
-                        q = q * s1 + b1;
-                        v[e] = epi_act(q, a.act1);
+                        for (int e = 0; e < 4; ++e) {
+                            float q = c[t][e] * se + 0.0f;
+                            q = q * e1s[t] + e1b[t];
+                            v[e] = epi_act(q, a.act1);
+                        }
+                        *reinterpret_cast<floatx4*>(hid + hc * a.HP + 16 * pg + 4 * g) = v;
                     }
-                    *reinterpret_cast<floatx4*>(hid + hc * a.HP + 16 * pg + 4 * g) = v;
                 }
             }
+            if (c0 + CHK < a.Ch) load_bwe(c0 + CHK);  // the next chunk's: lands under this chunk's other phases
         } else {
             for (int u = tid; u < CH * a.P; u += kIrThreads) {
                 const int hc = u / a.P, px = u - hc * a.P;
                 hid[hc * a.HP + px] = x_at(c0 + hc, px);
             }
         }
+#pragma unroll
+        for (int j = 0; j < CWPT; ++j) {
+            const int idx = tid + kIrThreads * j;
+            if (idx < CHK * 11) {
+                const int hc = idx / 11, k = idx - hc * 11;
+                cw[hc * kIrCw + k] = cwv[j];
+            }
+        }
         __syncthreads();
         // ---- depthwise 3x3 (pad 1, stride S), bn2 + act2, split -> d planes [Po][CHK]
-        const int noct = a.CHK / 8;
-        for (int u = tid; u < a.Po * noct; u += kIrThreads) {
+        for (int u = tid; u < a.Po * (CHK / 8); u += kIrThreads) {
             const int oc = u / a.Po, op = u - oc * a.Po;
             const int img = op / IMGo, r = op - img * IMGo;
             const int ry = r / a.Wo, ox = r - ry * a.Wo;
@@ -172,8 +241,7 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 const int hc = 8 * oc + e;
                 float v = 0.0f;
                 if (ok && hc < CH) {
-                    const int h = c0 + hc;
-                    const float* wk = a.wd + h * 9;
+                    const float* wk = cw + hc * kIrCw;
                     const float* hp = hid + hc * a.HP + img * IMG;
                     float s = 0.0f;
 #pragma unroll
@@ -188,7 +256,7 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                         }
                     }
                     float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
-                    q = q * (a.ps2 ? a.ps2[h] : 1.0f) + (a.pb2 ? a.pb2[h] : 0.0f);
+                    q = q * wk[9] + wk[10];
                     v = epi_act(q, a.act2);
                 }
                 b[e] = __float_as_uint(v);
@@ -204,13 +272,14 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
         // ---- project: the chunk's k-steps into this wave's units
         const int nks = (CH + 31) / 32;
 #pragma unroll
-        for (int i = 0; i < kIrUnits; ++i) {
+        for (int i = 0; i < UMAX; ++i) {
             const int u = wave + kIrWaves * i;
             if (u >= nunits) break;
-            const int opg = u / a.NTp, ot = u - opg * a.NTp;
-            for (int k2 = 0; k2 < nks; ++k2) {
-                const int ks = c0 / 32 + k2;
-                const bf16x8 bw = __builtin_bit_cast(bf16x8, a.wp[((int64_t)ks * a.NTp + ot) * 64 + lane]);
+            const int opg = u / a.NTp;
+#pragma unroll
+            for (int k2 = 0; k2 < KC; ++k2) {
+                if (k2 >= nks) break;
+                const bf16x8 bw = __builtin_bit_cast(bf16x8, bwp[i][k2]);
                 const int off = (16 * opg + pl) * drow + 16 * (4 * k2 + g);
 #pragma unroll
                 for (int p3 = 0; p3 < 3; ++p3) {
@@ -220,11 +289,12 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 }
             }
         }
+        if (c0 + CHK < a.Ch) load_bwp(c0 + CHK);
     }
 
     // ---- epilogue (conv_pw's): lane holds output channel 16 ot + pl, output pixels 16 opg + 4 g .. + 3
 #pragma unroll
-    for (int i = 0; i < kIrUnits; ++i) {
+    for (int i = 0; i < UMAX; ++i) {
         const int u = wave + kIrWaves * i;
         if (u >= nunits) break;
         const int opg = u / a.NTp, ot = u - opg * a.NTp;
@@ -249,22 +319,24 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
 // ------------------------------------------------------------------ planning --
 namespace {
 
-bool ir_geom(IrPlan& q, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout, int64_t S, bool expand,
-             int64_t R, int64_t G, int64_t CHK) {
+bool ir_geom(IrPlan& q, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t S, bool expand, int64_t R,
+             int64_t G, int KC) {
     const int64_t Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
     const int64_t RI = std::min<int64_t>(H, (R - 1) * S + 3);
     const int64_t P = G * RI * W, PG = (P + 15) / 16, Po = (G * R * Wo + 15) / 16 * 16;
     const int64_t xs = 32 * ((Cin + 31) / 32) + 4;
     const int64_t HP = 16 * PG + 4;  // 16-byte shift between channel rows: conflict-free float4 stores
+    const int64_t CHK = 32 * KC;
     const size_t xb = expand ? (size_t)16 * PG * xs * 4 : 0;
     const size_t hb = (size_t)CHK * HP * 4;
     const size_t db = (size_t)3 * Po * CHK * 2;
-    if (xb + hb + db > kIrLds) return false;
-    if (Po / 16 * ((Cout + 15) / 16) > kIrWaves * kIrUnits) return false;
+    const size_t cb = (size_t)CHK * kIrCw * 4;
+    if (xb + hb + db + cb > kIrLds) return false;
+    const int64_t units = Po / 16 * ((Cout + 15) / 16);
+    if (units > (int64_t)kIrWaves * ir_umax(KC)) return false;
     q.G = (int)G; q.R = (int)R; q.RI = (int)RI; q.nbands = (int)((Ho + R - 1) / R); q.CHK = (int)CHK;
     q.P = (int)P; q.PG = (int)PG; q.Po = (int)Po; q.HP = (int)HP; q.xs = (int)xs;
-    q.lds = xb + hb + db; q.off_hid = xb; q.off_dpl = xb + hb;
-    (void)Ch;
+    q.lds = xb + hb + db + cb; q.off_hid = xb; q.off_dpl = xb + hb; q.off_cw = xb + hb + db;
     return true;
 }
 
@@ -272,33 +344,36 @@ bool ir_geom(IrPlan& q, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t C
 
 // Geometry: whole images when one fits (G > 1 of them while a block has < 64 output pixels and
 // the grid keeps >= 512 blocks), else the tallest band of one image that fits the LDS budget and
-// the project unit cap; then the widest hidden chunk (up to 256 channels, no wider than the
-// hidden width) that still fits: small images get few, wide chunks (fewer barriers).
+// the project unit cap; then the widest chunk (KC = 8, 4, 2, 1 k-steps, no wider than the hidden
+// width) whose B fragments the waves can hold and whose buffers fit: small images get few, wide
+// chunks (fewer barriers).
 bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout, int64_t S,
              bool expand) {
     if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Ch <= 0 || Cout <= 0 || (S != 1 && S != 2)) return false;
-    if (Ch % 16 != 0 || (!expand && Ch != Cin) || Cin > 1024 || Ch > 4096 || Cout > 1024) return false;
+    if (Ch % 16 != 0 || (!expand && Ch != Cin) || Ch > 4096 || Cout > 1024) return false;
+    if (expand && Cin > 32 * kIrKse) return false;  // the expand B fragments live in registers
+    if (!expand && Cin > 4096) return false;
     if (N * Cin * H * W >= INT32_MAX || N * Cout * H * W >= INT32_MAX || N * Ch * H * W >= ((int64_t)1 << 40))
         return false;
     const int64_t Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
     IrPlan q{};
     bool found = false;
     int64_t R = Ho, G = 1;
-    for (; R >= 1 && !found; --R) found = ir_geom(q, Cin, H, W, Ch, Cout, S, expand, R, 1, 32);
+    for (; R >= 1 && !found; --R) found = ir_geom(q, Cin, H, W, Cout, S, expand, R, 1, 1);
     if (!found) return false;
     R = q.R;
     if (R == Ho) {
         while (G * Ho * Wo < 64 && N / (G * 2) >= 512) {
             IrPlan q2{};
-            if (!ir_geom(q2, Cin, H, W, Ch, Cout, S, expand, R, G * 2, 32)) break;
+            if (!ir_geom(q2, Cin, H, W, Cout, S, expand, R, G * 2, 1)) break;
             q = q2;
             G *= 2;
         }
     }
-    // the widest chunk that fits (q holds the 32-channel geometry, which does)
-    const int64_t chmax = (Ch + 31) / 32 * 32;
-    for (int64_t CHK = std::min<int64_t>(256, chmax); CHK > 32; CHK -= 32)
-        if (ir_geom(q, Cin, H, W, Ch, Cout, S, expand, R, G, CHK)) break;
+    // the widest chunk that fits (q holds the KC = 1 geometry, which does)
+    const int64_t ksteps = (Ch + 31) / 32;
+    for (int KC = 8; KC > 1; KC /= 2)
+        if (KC <= ksteps && ir_geom(q, Cin, H, W, Cout, S, expand, R, G, KC)) break;
     ip = q;
     ip.blocks = (N + G - 1) / G * q.nbands;
     return true;
@@ -310,8 +385,8 @@ hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int
     IrArgs a;
     a.N = N; a.Cin = Cin; a.H = H; a.W = W; a.Ch = Ch; a.Cout = Cout; a.S = S;
     a.Ho = (H - 1) / S + 1; a.Wo = (W - 1) / S + 1;
-    a.G = ip.G; a.R = ip.R; a.RI = ip.RI; a.nbands = ip.nbands; a.CHK = ip.CHK;
-    a.KSe = (Cin + 31) / 32; a.NTe = (Ch + 15) / 16; a.NTp = (Cout + 15) / 16;
+    a.G = ip.G; a.R = ip.R; a.RI = ip.RI; a.nbands = ip.nbands;
+    a.KSe = (Cin + 31) / 32; a.NTe = (Ch + 15) / 16; a.KSp = (Ch + 31) / 32; a.NTp = (Cout + 15) / 16;
     a.xs = ip.xs; a.P = ip.P; a.PG = ip.PG; a.Po = ip.Po; a.HP = ip.HP;
     a.we = reinterpret_cast<const uint4*>(we);
     a.we_scale = we_scale;
@@ -323,13 +398,23 @@ hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int
     a.res = e.res;
     a.off_hid = (int)ip.off_hid;
     a.off_dpl = (int)ip.off_dpl;
-    if (ip.lds > 64 * 1024) {
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv_ir),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kIrLds);
-        if (attr != hipSuccess) return attr;
+    a.off_cw = (int)ip.off_cw;
+    auto go = [&](auto kern) -> hipError_t {
+        if (ip.lds > 64 * 1024) {
+            const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kIrLds);
+            if (attr != hipSuccess) return attr;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
+        return hipGetLastError();
+    };
+    switch (ip.CHK) {
+        case 32: return go(conv_ir<1>);
+        case 64: return go(conv_ir<2>);
+        case 128: return go(conv_ir<4>);
+        case 256: return go(conv_ir<8>);
+        default: return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(conv_ir, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
-    return hipGetLastError();
 }
 
 }  // namespace po2q

@@ -195,7 +195,7 @@ hipError_t launch_conv_bf16x3_dma(const ConvPlan& p, const float* x, const uint1
 // eval BN / activations / identity residual, hidden activations in LDS.
 struct IrPlan {
     int G, R, RI, nbands, CHK, P, PG, Po, HP, xs;
-    size_t lds, off_hid, off_dpl;
+    size_t lds, off_hid, off_dpl, off_cw;
     int64_t blocks;
 };
 struct IrEpi {

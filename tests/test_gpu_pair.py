@@ -221,11 +221,13 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     forms = [{}, dict(act1="relu", act2="relu6", **e)]
     if C == 16:  # the identity residual read from the x ring (BasicBlock form and the general epilogue)
         forms += [dict(act1="relu", act2="relu", residual=x, **e), dict(act1="relu6", act2="silu", residual=x, **e)]
+    outs = []
     for kw in forms:
         monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
         ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
         monkeypatch.setenv("PO2Q_PAIR_MW", str(pd))
         y = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
         assert torch.equal(y, ref), (pd, shape, sorted(kw))
-    t = torch_chain(x, w1, w2, e, "relu", "relu6", None)
-    assert nerr(y, t) <= CONV_TOL
+        outs.append(y)
+    t = torch_chain(x, w1, w2, e, "relu", "relu6", None)  # forms[1]
+    assert nerr(outs[1], t) <= CONV_TOL

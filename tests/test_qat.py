@@ -101,6 +101,15 @@ def test_graphed_train_step_equals_eager_steps():
     from one HIP graph) against the same steps run eagerly from the same initial
     state: the warm-up leaves no trace and every replay is the eager step's arithmetic."""
     torch.backends.cudnn.benchmark = False
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # the unquantized stem's MIOpen backward, run to run
+    try:
+        _graphed_vs_eager()
+    finally:
+        torch.backends.cudnn.deterministic = det
+
+
+def _graphed_vs_eager():
     g = torch.Generator().manual_seed(11)
     batches = [(torch.randn(16, 3, 32, 32, generator=g).to(DEV), torch.randint(0, 10, (16,), generator=g).to(DEV))
                for _ in range(4)]
@@ -129,7 +138,9 @@ def test_graphed_train_step_equals_eager_steps():
     bad = []
     for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
         if a.is_floating_point():
-            if not torch.allclose(a, b, rtol=1e-4, atol=1e-6):
+            # the eager step against itself sets the floor (any run-to-run noise left in a library
+            # backward); the replay must be as close to the eager step as the eager step to itself
+            if not torch.allclose(a, b, rtol=1e-4, atol=max(1e-6, 2 * noise[k])):
                 bad.append((k, (a - b).abs().max().item(), a.abs().max().item(), noise[k]))
         elif not torch.equal(a, b):
             bad.append((k, "int", None))
