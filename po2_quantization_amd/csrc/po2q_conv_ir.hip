@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "po2q_epi.h"
 #include "po2q_internal.h"
@@ -46,6 +47,7 @@ namespace {
 constexpr int kIrThreads = 512;  // 8 waves
 constexpr int kIrWaves = kIrThreads / 64;
 constexpr int kIrKse = 5;     // expand k-steps held in registers: Cin <= 160
+constexpr int kIrBatch = 8;   // independent global loads per thread in the staging loops
 constexpr int kIrCw = 12;     // staged depthwise parameters per hidden channel: 9 taps, bn scale, shift, pad
 constexpr size_t kIrLds = 150 * 1024;
 // project units one wave holds B fragments for, by k-steps per chunk (<= 16 fragments = 64 VGPRs)
@@ -68,6 +70,11 @@ struct IrArgs {
     const float* res;      // residual [N, Cout, Ho, Wo] or NULL
     int off_hid, off_dpl, off_cw;  // LDS byte offsets
 };
+
+// Block barrier over LDS only: every LDS access of this wave retired, then s_barrier.  Not
+// __syncthreads: its release fence also waits for every global load in flight (vmcnt(0)), which would
+// serialise the register prefetches of the next chunk's weights with this chunk's phases.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // LDS: x [16 PG][xs] fp32 (expand only) | hidden chunk [CHK][HP] fp32 | d planes 3 x [Po][CHK] bf16 |
 // the chunk's depthwise parameters [CHK][12] fp32.  KC: project k-steps per chunk (CHK = 32 KC).
@@ -135,12 +142,28 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
         if (img >= a.G || n0 + img >= a.N || iy > iy1 || c >= a.Cin) return 0.0f;
         return x[(((int64_t)(n0 + img) * a.Cin + c) * a.H + iy) * a.W + ix];
     };
+    // global -> LDS staging, kIrBatch independent loads in flight per thread (a loop of one load
+    // and one LDS store per iteration pays a full memory latency per element)
+    auto stage = [&](int total, auto&& src, auto&& dst) __attribute__((always_inline)) {
+        for (int base = tid; base < total; base += kIrThreads * kIrBatch) {
+            float v[kIrBatch];
+#pragma unroll
+            for (int j = 0; j < kIrBatch; ++j) {
+                const int u = base + kIrThreads * j;
+                v[j] = u < total ? src(u) : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < kIrBatch; ++j) {
+                const int u = base + kIrThreads * j;
+                if (u < total) dst(u, v[j]);
+            }
+        }
+    };
     if (expand) {
         const int cinp = 32 * a.KSe, P16 = 16 * a.PG;
-        for (int u = tid; u < P16 * cinp; u += kIrThreads) {
-            const int c = u / P16, px = u - c * P16;
-            xl[px * a.xs + c] = x_at(c, px);
-        }
+        stage(
+            P16 * cinp, [&](int u) { return x_at(u / P16, u - (u / P16) * P16); },
+            [&](int u, float v) { xl[(u - (u / P16) * P16) * a.xs + u / P16] = v; });
     }
     const float se = expand ? *a.we_scale : 1.0f;
     const float sp = *a.wp_scale;
@@ -165,7 +188,7 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
             }
             cwv[j] = v;
         }
-        __syncthreads();  // x staged / the previous chunk's depthwise reads of hid and cw retired
+        lds_barrier();  // x staged / the previous chunk's depthwise reads of hid and cw retired
         // ---- expand (or copy x) -> hid [CH][HP] fp32
         if (expand) {
             const int ntile = CH / 16, t0 = 2 * tp, nt = min(2, ntile - t0);
@@ -214,10 +237,9 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
             }
             if (c0 + CHK < a.Ch) load_bwe(c0 + CHK);  // the next chunk's: lands under this chunk's other phases
         } else {
-            for (int u = tid; u < CH * a.P; u += kIrThreads) {
-                const int hc = u / a.P, px = u - hc * a.P;
-                hid[hc * a.HP + px] = x_at(c0 + hc, px);
-            }
+            stage(
+                CH * a.P, [&](int u) { return x_at(c0 + u / a.P, u - (u / a.P) * a.P); },
+                [&](int u, float v) { hid[(u / a.P) * a.HP + u - (u / a.P) * a.P] = v; });
         }
 #pragma unroll
         for (int j = 0; j < CWPT; ++j) {
@@ -227,39 +249,46 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 cw[hc * kIrCw + k] = cwv[j];
             }
         }
-        __syncthreads();
+        lds_barrier();
         // ---- depthwise 3x3 (pad 1, stride S), bn2 + act2, split -> d planes [Po][CHK]
+        // branch-free: the 9 tap offsets of the output pixel (clamped into the band, a select zeroes
+        // the padding taps) are shared by its 8 channels, so every LDS read is unconditional and
+        // the 72 of a unit are independent
         for (int u = tid; u < a.Po * (CHK / 8); u += kIrThreads) {
             const int oc = u / a.Po, op = u - oc * a.Po;
             const int img = op / IMGo, r = op - img * IMGo;
             const int ry = r / a.Wo, ox = r - ry * a.Wo;
-            const int oy = oy0 + ry;
+            const int oy = oy0 + min(ry, Rb - 1);
             const bool ok = img < a.G && ry < Rb;
+            int toff[9];
+            bool tin[9];
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const int iy = oy * a.S - 1 + rr;
+                const int iyc = min(max(iy, iy0), iy1);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int ix = ox * a.S - 1 + t;
+                    toff[rr * 3 + t] = min(img, a.G - 1) * IMG + (iyc - iy0) * a.W + min(max(ix, 0), a.W - 1);
+                    tin[rr * 3 + t] = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                }
+            }
             uint32_t b[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int hc = 8 * oc + e;
-                float v = 0.0f;
-                if (ok && hc < CH) {
-                    const float* wk = cw + hc * kIrCw;
-                    const float* hp = hid + hc * a.HP + img * IMG;
-                    float s = 0.0f;
+                const float* wk = cw + hc * kIrCw;
+                const float* hp = hid + hc * a.HP;
+                float s = 0.0f;
 #pragma unroll
-                    for (int rr = 0; rr < 3; ++rr) {
-                        const int iy = oy * a.S - 1 + rr;
-                        const bool rok = iy >= 0 && iy < a.H;
-#pragma unroll
-                        for (int t = 0; t < 3; ++t) {
-                            const int ix = ox * a.S - 1 + t;
-                            const float hv = (rok && ix >= 0 && ix < a.W) ? hp[(iy - iy0) * a.W + ix] : 0.0f;
-                            s = fmaf(hv, wk[rr * 3 + t], s);
-                        }
-                    }
-                    float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
-                    q = q * wk[9] + wk[10];
-                    v = epi_act(q, a.act2);
+                for (int k = 0; k < 9; ++k) {
+                    const float raw = hp[toff[k]];
+                    s = fmaf(tin[k] ? raw : 0.0f, wk[k], s);
                 }
-                b[e] = __float_as_uint(v);
+                float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
+                q = q * wk[9] + wk[10];
+                const float v = epi_act(q, a.act2);
+                b[e] = (ok && hc < CH) ? __float_as_uint(v) : 0u;
             }
             uint4 hi, mid, lo;
             split3(b, hi, mid, lo);
@@ -268,7 +297,7 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
             *reinterpret_cast<uint4*>(dpl + dplane + off) = mid;
             *reinterpret_cast<uint4*>(dpl + 2 * dplane + off) = lo;
         }
-        __syncthreads();
+        lds_barrier();
         // ---- project: the chunk's k-steps into this wave's units
         const int nks = (CH + 31) / 32;
 #pragma unroll
@@ -362,8 +391,11 @@ bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t C
     for (; R >= 1 && !found; --R) found = ir_geom(q, Cin, H, W, Cout, S, expand, R, 1, 1);
     if (!found) return false;
     R = q.R;
+    // PO2Q_IR_MINBLOCKS (A/B knob): the fewest blocks image grouping may leave (default 512)
+    int64_t minblocks = 512;
+    if (const char* e = getenv("PO2Q_IR_MINBLOCKS")) minblocks = std::max(1, atoi(e));
     if (R == Ho) {
-        while (G * Ho * Wo < 64 && N / (G * 2) >= 512) {
+        while (G * Ho * Wo < 64 && N / (G * 2) >= minblocks) {
             IrPlan q2{};
             if (!ir_geom(q2, Cin, H, W, Cout, S, expand, R, G * 2, 1)) break;
             q = q2;

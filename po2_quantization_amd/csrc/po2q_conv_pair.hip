@@ -653,7 +653,8 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         __syncthreads();  // scratch reads done: zero the intermediate planes (padding columns, zero slots)
         for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
             reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
-        if (lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+        if (lane < 3 && wave < nw)  // MW: the memory wave has no planes (wave nw's would be wl2 / beyond)
+            *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
         // step 0's barrier publishes the zeros (and wl2)
     }
     // static priority for the younger wave of each SIMD (MI355X_MICROARCH two-waves item 4)
@@ -1187,6 +1188,13 @@ void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C
     prio = C == 16 ? 1 : 0;
     halves = 0;
     stg = 0;
+    // C = 32 stores 64-byte half lines per wave (16 columns): non-temporal, the halves of a line
+    // from neighbouring waves reach HBM as two partial writes (1.35x the output bytes,
+    // r03_pmc_pair32_v7.json).  PO2Q_PAIR_C32_TS=1: temporal stores, merged in L2 (1.00x).
+    if (C == 32) {
+        const char* ts = getenv("PO2Q_PAIR_C32_TS");
+        if (ts && ts[0] == '1') nts = 2;
+    }
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
         int v = atoi(e);
         stg = v >= 20000 ? 2 : (v >= 10000 ? 1 : 0);  // + 10000: the stagger kernel (STG) where no residual is
