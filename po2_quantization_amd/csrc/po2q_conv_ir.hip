@@ -36,6 +36,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#ifdef PO2Q_IR_STAMPS
+#include <cstdio>
+#include <vector>
+#endif
 
 #include "po2q_epi.h"
 #include "po2q_internal.h"
@@ -50,8 +54,9 @@ constexpr int kIrKse = 5;     // expand k-steps held in registers: Cin <= 160
 constexpr int kIrBatch = 8;   // independent global loads per thread in the staging loops
 constexpr int kIrCw = 12;     // staged depthwise parameters per hidden channel: 9 taps, bn scale, shift, pad
 constexpr size_t kIrLds = 150 * 1024;
-// project units one wave holds B fragments for, by k-steps per chunk (<= 16 fragments = 64 VGPRs)
-constexpr int ir_umax(int kc) { return kc >= 8 ? 2 : (kc >= 4 ? 4 : 8); }
+// project units one wave holds B fragments for, by k-steps per chunk (<= 8 fragments = 32 VGPRs:
+// the prefetched fragments are live through the depthwise phase, whose tap reads need the room)
+constexpr int ir_umax(int kc) { return kc >= 8 ? 1 : (kc >= 4 ? 2 : (kc >= 2 ? 4 : 8)); }
 }  // namespace
 
 struct IrArgs {
@@ -69,7 +74,29 @@ struct IrArgs {
     int act1, act2, act3;
     const float* res;      // residual [N, Cout, Ho, Wo] or NULL
     int off_hid, off_dpl, off_cw;  // LDS byte offsets
+    unsigned* stamps;  // PO2Q_IR_STAMPS diagnostic builds only: per (block, wave) phase cycle sums
 };
+
+// Diagnostic build (-DPO2Q_IR_STAMPS, `make irstamps`): s_memtime phase stamps, never in the
+// product build.  Phases: 0 prologue, 1 barrier A, 2 expand, 3 expand prefetch issue, 4 depthwise
+// parameters to LDS (their load wait), 5 barrier B, 6 depthwise, 7 barrier C, 8 project,
+// 9 project prefetch issue, 10 epilogue.
+[[maybe_unused]] constexpr int kIrPhases = 11;
+#ifdef PO2Q_IR_STAMPS
+#define IRS(i)                                                                           \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        ph_[i] += (unsigned)(t_ - tprev_);                                               \
+        tprev_ = t_;                                                                     \
+    } while (0)
+#else
+#define IRS(i) \
+    do {       \
+    } while (0)
+#endif
 
 // Block barrier over LDS only: every LDS access of this wave retired, then s_barrier.  Not
 // __syncthreads: its release fence also waits for every global load in flight (vmcnt(0)), which would
@@ -83,6 +110,11 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
     constexpr int CHK = 32 * KC;
     constexpr int UMAX = ir_umax(KC);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+#ifdef PO2Q_IR_STAMPS
+    unsigned ph_[kIrPhases] = {};
+    unsigned long long tprev_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, pl = lane & 15;
@@ -188,7 +220,9 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
             }
             cwv[j] = v;
         }
+        IRS(0);
         lds_barrier();  // x staged / the previous chunk's depthwise reads of hid and cw retired
+        IRS(1);
         // ---- expand (or copy x) -> hid [CH][HP] fp32
         if (expand) {
             const int ntile = CH / 16, t0 = 2 * tp, nt = min(2, ntile - t0);
@@ -235,7 +269,9 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                     }
                 }
             }
+            IRS(2);
             if (c0 + CHK < a.Ch) load_bwe(c0 + CHK);  // the next chunk's: lands under this chunk's other phases
+            IRS(3);
         } else {
             stage(
                 CH * a.P, [&](int u) { return x_at(c0 + u / a.P, u - (u / a.P) * a.P); },
@@ -249,7 +285,9 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 cw[hc * kIrCw + k] = cwv[j];
             }
         }
+        IRS(4);
         lds_barrier();
+        IRS(5);
         // ---- depthwise 3x3 (pad 1, stride S), bn2 + act2, split -> d planes [Po][CHK]
         // branch-free: the 9 tap offsets of the output pixel (clamped into the band, a select zeroes
         // the padding taps) are shared by its 8 channels, so every LDS read is unconditional and
@@ -274,21 +312,32 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 }
             }
             uint32_t b[8];
+            // two channels per batch: their 18 tap reads and 6 parameter reads are all issued
+            // before the first FMA (one LDS round trip per batch, not one per tap)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int hc = 8 * oc + e;
-                const float* wk = cw + hc * kIrCw;
-                const float* hp = hid + hc * a.HP;
-                float s = 0.0f;
+            for (int e0 = 0; e0 < 8; e0 += 2) {
+                float hv[2][9];
+                floatx4 wv[2][3];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    const float raw = hp[toff[k]];
-                    s = fmaf(tin[k] ? raw : 0.0f, wk[k], s);
+                for (int e = 0; e < 2; ++e) {
+                    const int hc = 8 * oc + e0 + e;
+                    const float* hp = hid + hc * a.HP;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) hv[e][k] = hp[toff[k]];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) wv[e][j] = *reinterpret_cast<const floatx4*>(cw + hc * kIrCw + 4 * j);
                 }
-                float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
-                q = q * wk[9] + wk[10];
-                const float v = epi_act(q, a.act2);
-                b[e] = (ok && hc < CH) ? __float_as_uint(v) : 0u;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int hc = 8 * oc + e0 + e;
+                    float s = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) s = fmaf(tin[k] ? hv[e][k] : 0.0f, wv[e][k >> 2][k & 3], s);
+                    float q = s + 0.0f;  // conv_dw3's epilogue (no bias)
+                    q = q * wv[e][2][1] + wv[e][2][2];
+                    const float v = epi_act(q, a.act2);
+                    b[e0 + e] = (ok && hc < CH) ? __float_as_uint(v) : 0u;
+                }
             }
             uint4 hi, mid, lo;
             split3(b, hi, mid, lo);
@@ -297,7 +346,9 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
             *reinterpret_cast<uint4*>(dpl + dplane + off) = mid;
             *reinterpret_cast<uint4*>(dpl + 2 * dplane + off) = lo;
         }
+        IRS(6);
         lds_barrier();
+        IRS(7);
         // ---- project: the chunk's k-steps into this wave's units
         const int nks = (CH + 31) / 32;
 #pragma unroll
@@ -318,31 +369,49 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
                 }
             }
         }
+        IRS(8);
         if (c0 + CHK < a.Ch) load_bwp(c0 + CHK);
+        IRS(9);
     }
 
-    // ---- epilogue (conv_pw's): lane holds output channel 16 ot + pl, output pixels 16 opg + 4 g .. + 3
+    // ---- epilogue (conv_pw's): lane holds output channel 16 ot + pl, output pixels 16 opg + 4 g .. + 3.
+    // Two passes: every residual and BN load of the wave first, then the stores (one round trip).
+    // Indices fit 32 bits (ir_plan: N Cout H W < 2^31).
+    int yi[UMAX][4];
+    float rv[UMAX][4], s3[UMAX], b3[UMAX];
 #pragma unroll
     for (int i = 0; i < UMAX; ++i) {
         const int u = wave + kIrWaves * i;
-        if (u >= nunits) break;
         const int opg = u / a.NTp, ot = u - opg * a.NTp;
         const int k = 16 * ot + pl;
-        if (k >= a.Cout) continue;
-        const float s3 = a.ps3 ? a.ps3[k] : 1.0f, b3 = a.pb3 ? a.pb3[k] : 0.0f;
+        const bool kok = u < nunits && k < a.Cout;
+        s3[i] = (kok && a.ps3) ? a.ps3[k] : 1.0f;
+        b3[i] = (kok && a.pb3) ? a.pb3[k] : 0.0f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int op = 16 * opg + 4 * g + e;
             const int img = op / IMGo, r = op - img * IMGo;
             const int ry = r / a.Wo, ox = r - ry * a.Wo;
-            if (img >= a.G || n0 + img >= a.N || ry >= Rb) continue;
-            const int64_t yi = (((int64_t)(n0 + img) * a.Cout + k) * a.Ho + oy0 + ry) * a.Wo + ox;
-            float v = acc[i][e] * sp + 0.0f;
-            v = v * s3 + b3;
-            if (a.res) v += a.res[yi];
-            y[yi] = epi_act(v, a.act3);
+            const bool ok = kok && img < a.G && n0 + img < a.N && ry < Rb;
+            yi[i][e] = ok ? (((n0 + img) * a.Cout + k) * a.Ho + oy0 + ry) * a.Wo + ox : -1;
+            rv[i][e] = (ok && a.res) ? a.res[yi[i][e]] : 0.0f;
         }
     }
+#pragma unroll
+    for (int i = 0; i < UMAX; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = acc[i][e] * sp + 0.0f;
+            v = v * s3[i] + b3[i];
+            if (a.res) v += rv[i][e];
+            if (yi[i][e] >= 0) y[yi[i][e]] = epi_act(v, a.act3);
+        }
+    }
+#ifdef PO2Q_IR_STAMPS
+    IRS(10);
+    if (lane == 0 && a.stamps)
+        for (int i = 0; i < kIrPhases; ++i) a.stamps[((size_t)blockIdx.x * kIrWaves + wave) * kIrPhases + i] = ph_[i];
+#endif
 }
 
 // ------------------------------------------------------------------ planning --
@@ -431,12 +500,39 @@ hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int
     a.off_hid = (int)ip.off_hid;
     a.off_dpl = (int)ip.off_dpl;
     a.off_cw = (int)ip.off_cw;
+    a.stamps = nullptr;
     auto go = [&](auto kern) -> hipError_t {
         if (ip.lds > 64 * 1024) {
             const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kIrLds);
             if (attr != hipSuccess) return attr;
         }
+#ifdef PO2Q_IR_STAMPS
+        const size_t nst = (size_t)ip.blocks * kIrWaves * kIrPhases;
+        if (getenv("PO2Q_STAMPS") && hipMalloc(&a.stamps, nst * 4) == hipSuccess) {
+            (void)hipMemsetAsync(a.stamps, 0, nst * 4, s);
+            hipLaunchKernelGGL(kern, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
+            std::vector<unsigned> h(nst);
+            (void)hipStreamSynchronize(s);
+            (void)hipMemcpy(h.data(), a.stamps, nst * 4, hipMemcpyDeviceToHost);
+            (void)hipFree(a.stamps);
+            fprintf(stderr, "[po2q ir stamps] N=%d Cin=%d H=%d Ch=%d Cout=%d S=%d CHK=%d G=%d blocks=%lld, cycles/block by wave:\n",
+                    N, Cin, H, Ch, Cout, S, ip.CHK, ip.G, (long long)ip.blocks);
+            for (int w = 0; w < kIrWaves; ++w) {
+                double tot = 0;
+                fprintf(stderr, "  wave %d:", w);
+                for (int i = 0; i < kIrPhases; ++i) {
+                    double sum = 0;
+                    for (int64_t b = 0; b < ip.blocks; ++b) sum += h[((size_t)b * kIrWaves + w) * kIrPhases + i];
+                    sum /= (double)ip.blocks;
+                    tot += sum;
+                    fprintf(stderr, " %d:%.0f", i, sum);
+                }
+                fprintf(stderr, " total %.0f\n", tot);
+            }
+            return hipGetLastError();
+        }
+#endif
         hipLaunchKernelGGL(kern, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
         return hipGetLastError();
     };

@@ -1316,13 +1316,19 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.halves = halves;
     a.stg = stg;
     a.stamps = nullptr;
-    // PO2Q_PAIR_MW = PD (3..6): the memory-wave kernel with a PD-slot x ring (A/B knob)
+    // The memory-wave kernel with a PD-slot x ring: the default at C = 16 (PD 5; 6 for the identity
+    // residual read from the ring): 0.4286 vs 0.4385 ms for the plain pair 16 @224 bs 256, 4
+    // interleaved rounds (profiles/r04_pair_mw_ab.jsonl); at C = 32 no gain (0.3401 vs 0.3394).
+    // PO2Q_PAIR_MW = PD (3..6) selects the ring depth, 0 the one-role kernel (A/B knob).
     a.mw = 0;
-    if (const char* mv = getenv("PO2Q_PAIR_MW")) {
+    const char* mv = getenv("PO2Q_PAIR_MW");
+    if (!mv && C == 16 && !getenv("PO2Q_PAIR_VARIANT")) mv = "5";
+    if (mv) {
         const int d = atoi(mv);
         // with a residual: only the identity shortcut (residual == x), from a 6-slot ring
         const bool ring_res = residual != nullptr && residual == x && C == 16;
-        if (d >= 3 && d <= 6 && (!residual || ring_res)) {
+        const bool seven = W > 6 * (512 / C);  // the memory-wave kernel exists for 7 compute waves only
+        if (d >= 3 && d <= 6 && seven && (!residual || ring_res)) {
             a.mw = 1;
             pd = residual ? 6 : d;
             nts = 3;  // with the ring residual no x row is re-read from memory: non-temporal loads

@@ -198,7 +198,7 @@ def test_model_forward_ir_fusion(name, image, q, bits, monkeypatch):
     real = _lib.qconv2d_ir
     monkeypatch.setattr(_lib, "qconv2d_ir", lambda *a, **k: calls.append(1) or real(*a, **k))
     with torch.no_grad():
-        monkeypatch.setattr(qc, "IR_FUSION", False)
+        monkeypatch.setattr(qc, "IR_FUSION", False)  # (the default)
         ref = m(x)
         ref2 = m(x)
         monkeypatch.setattr(qc, "IR_FUSION", True)

@@ -64,7 +64,7 @@ def test_pair_chain_vs_torch(shape, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(2, 20, 32, 16), (2, 23, 224, 16), (3, 37, 68, 16), (2, 20, 32, 32),
-                                   (2, 23, 112, 32)])
+                                   (2, 23, 112, 32), (2, 11, 160, 16), (1, 7, 200, 16)])
 @pytest.mark.parametrize("acts,with_res", [(("relu", "relu"), True), (("relu", "relu"), False),
                                            (("relu6", "silu"), True), (("none", "relu"), True)])
 def test_pair_block_epilogue_vs_torch(shape, acts, with_res):
