@@ -34,6 +34,9 @@
 #include <vector>
 
 #include "../../include/po2q.h"
+#ifdef PO2Q_CHAIN_STAMPS
+#include <cstdio>
+#endif
 #include "po2q_epi.h"
 #include "po2q_internal.h"
 #include "po2q_x3_dev.h"
@@ -95,8 +98,28 @@ struct ChainArgs {
     int H, W, L;
     int PW, PL, ZO;
     int res0;             // 1: x itself is a later layer's residual: hold it
+    unsigned* stamps;     // PO2Q_CHAIN_STAMPS diagnostic builds only: per (block, wave) phase cycle sums
     ChainLayer layer[kChainMax];
 };
+
+// Diagnostic build (-DPO2Q_CHAIN_STAMPS, `make chainstamps`): s_memtime phase stamps, never in the
+// product build.  Phases: 0 prologue (x split), 1 MFMA, 2 barrier after the MFMAs, 3 epilogue,
+// 4 barrier after the epilogue.
+#ifdef PO2Q_CHAIN_STAMPS
+#define CHS(i)                                                                           \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        ph_[i] += (unsigned)(t_ - tprev_);                                               \
+        tprev_ = t_;                                                                     \
+    } while (0)
+#else
+#define CHS(i) \
+    do {       \
+    } while (0)
+#endif
 
 // Exact 3-way split of 4 fp32 values (split3 of po2q_x3_dev.h, 4 lanes of it): 4 bf16 per plane.
 __device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mid, uint2& lo) {
@@ -134,6 +157,11 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     constexpr int NT = C / 16;                      // output tiles
     constexpr int WPT = (kChainThreads / 64) / NT;  // waves per output tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+#ifdef PO2Q_CHAIN_STAMPS
+    unsigned ph_[5] = {};
+    unsigned long long tprev_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n = blockIdx.x;
@@ -330,6 +358,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         floatx4 acc[MG];
 #pragma unroll
         for (int gi = 0; gi < MG; ++gi) acc[gi] = floatx4{0.f, 0.f, 0.f, 0.f};
+        CHS(0);
         if constexpr (C == 16) {
             mma16(acc);
         } else {
@@ -360,6 +389,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
 
         // the next layer's B fragments go out now (the last layer reloads its own: no branch, so
         // the epilogue's wait for this layer's constants stays a counted vmcnt, not vmcnt(0))
+        CHS(1);
         const bool last = l + 1 == a.L;
         const int act = ly.act, res_add = ly.res_add, keep = ly.keep;
         load_bw(a.layer[last ? l : l + 1]);
@@ -370,6 +400,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         }
+        CHS(2);
 
         // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p
 #pragma unroll
@@ -398,10 +429,16 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
             }
         }
+        CHS(3);
         // the next layer's input planes are complete (the block's own LDS writes: lgkmcnt)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        CHS(4);
     }
+#ifdef PO2Q_CHAIN_STAMPS
+    if (lane == 0 && a.stamps)
+        for (int i = 0; i < 5; ++i) a.stamps[((size_t)blockIdx.x * 8 + wave) * 5 + i] = ph_[i];
+#endif
 }
 
 // ------------------------------------------------------------------- host side --
@@ -550,6 +587,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     for (int l = 0; l < n_layers; ++l)
         if (res_from && res_from[l] >= 0) used[res_from[l]] = 1;
     ChainArgs a{};
+    a.stamps = nullptr;
     a.H = (int)H; a.W = (int)W; a.L = n_layers;
     a.PW = (int)W + 2;
     a.PL = (int)chain_plane(C, H, W);
@@ -580,6 +618,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     const int64_t wpt = (kChainThreads / 64) / (C / 16);
     const bool full = !(variant & 1) && (H * W) % 16 == 0 && (H * W / 16) % wpt == 0;
     // the exact-fit forms (FULL) for the CIFAR stages, the checked forms for everything else
+    auto launch = [&](const ChainArgs& a) -> bool {
 #define PO2Q_CH(c, m, w)                                                                               \
     if (C == c && mg <= m && w8 == w) {                                                                \
         if (c == 16 && (variant & 2)) {                                                                \
@@ -601,15 +640,43 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     PO2Q_CH(16, 2, false) PO2Q_CH(16, 4, false) PO2Q_CH(16, 8, false)
     PO2Q_CH(32, 2, false) PO2Q_CH(32, 4, false)
     PO2Q_CH(64, 2, true) PO2Q_CH(64, 4, true) PO2Q_CH(64, 2, false) PO2Q_CH(64, 4, false) {
+        return false;
+    }
+#undef PO2Q_CH
+        return true;
+    };
+    if (!launch(a)) {
         set_error("po2q: chain: no kernel for this shape");
         return PO2Q_ERR_INVALID;
     }
-#undef PO2Q_CH
     he = hipGetLastError();
     if (he != hipSuccess) {
         set_error(std::string("po2q: chain launch: ") + hipGetErrorString(he));
         return PO2Q_ERR_HIP;
     }
+#ifdef PO2Q_CHAIN_STAMPS
+    if (getenv("PO2Q_STAMPS") && !a.stamps) {  // once more with the stamp buffer, summed per phase
+        const size_t nst = (size_t)N * 8 * 5;
+        if (hipMalloc(&a.stamps, nst * 4) == hipSuccess) {
+            (void)hipMemsetAsync(a.stamps, 0, nst * 4, s);
+            launch(a);
+            std::vector<unsigned> h(nst);
+            (void)hipStreamSynchronize(s);
+            (void)hipMemcpy(h.data(), a.stamps, nst * 4, hipMemcpyDeviceToHost);
+            (void)hipFree(a.stamps);
+            double ph[5] = {0, 0, 0, 0, 0};
+            for (int64_t b = 0; b < N; ++b)
+                for (int w = 0; w < 8; ++w)
+                    for (int i = 0; i < 5; ++i) ph[i] += h[((size_t)b * 8 + w) * 5 + i];
+            fprintf(stderr, "[po2q chain stamps] C=%lld H=%lld W=%lld L=%d db=%d: cycles per layer per wave:", (long long)C,
+                    (long long)H, (long long)W, n_layers, db ? 1 : 0);
+            const char* names[5] = {"prologue", "mfma", "bar1", "epilogue", "bar2"};
+            for (int i = 0; i < 5; ++i)
+                fprintf(stderr, " %s %.0f", names[i], ph[i] / (double)(N * 8) / (i ? n_layers : 1));
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
     return PO2Q_OK;
 }
 

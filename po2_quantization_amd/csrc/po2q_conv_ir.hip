@@ -43,6 +43,7 @@
 
 #include "po2q_epi.h"
 #include "po2q_internal.h"
+#include "po2q_rows_dev.h"
 #include "po2q_x3_dev.h"
 
 namespace po2q {
@@ -414,6 +415,225 @@ __global__ __launch_bounds__(kIrThreads) void conv_ir(const float* __restrict__ 
 #endif
 }
 
+// ------------------------------------------------------------------ small images --
+// conv_ir_small: the block for images of at most 16 pixels (MobileNetV2 @32 from its 4x4 stage on:
+// 13 of 17 blocks).  There the chunked kernel above runs ~15 chunks of a few dozen MFMAs, each
+// behind three block barriers, and its 16-row pixel tiles hold 1-4 real pixels.  Here a block owns
+// G images whose G H W <= 16 pixels fill ONE 16-row MFMA tile, and the hidden channels are split
+// over the waves in 32-channel slices that each wave runs end to end with no block barrier:
+//   expand (A = the block's pre-split x planes, B = the slice's two expand tiles) -> bn1 + act1 ->
+//   the wave's own LDS [32 ch][16 px] -> depthwise 3x3 (lane = channel, 8 output pixels) -> bn2 +
+//   act2 -> exact split -> the wave's own bf16 planes [16 px][32 ch] -> project: one k-step into
+//   the wave's NTW output tiles (partial sums over its slices, in registers).
+// The next slice's B fragments and depthwise parameters are loaded right after their phase used
+// the current ones.  At the end the partial sums of the waves meet in LDS and are added in a fixed
+// wave order (deterministic), then bn3 (+ the residual) + act3 and the store.  With more than NTW
+// output tiles the waves form TG groups, each over its own tiles (the expand / depthwise work of a
+// slice is then repeated per group: it is the small part at these sizes).
+constexpr int kIrsWave = 5120;  // per-wave LDS: hidden [32][16] fp32 (2 KiB) + 3 bf16 planes [16][32] (3 KiB)
+
+template <int NTW>
+__global__ __launch_bounds__(kIrThreads) void conv_ir_small(const float* __restrict__ x, float* __restrict__ y,
+                                                            IrArgs a, int TG) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, pl = lane & 15;
+    const int n0 = blockIdx.x * a.G;
+    const int HW = a.H * a.W, HWo = a.Ho * a.Wo;
+    const int P = a.G * HW, Po = a.G * HWo;  // <= 16 each
+    const int cinp = 32 * a.KSe;
+    const int xplane = 16 * cinp * 2;
+    unsigned char* xpl = lds;
+    float* hidw = reinterpret_cast<float*>(lds + 3 * xplane + wave * kIrsWave);
+    unsigned char* dplw = lds + 3 * xplane + wave * kIrsWave + 2048;
+    constexpr uint4 z4 = {0u, 0u, 0u, 0u};
+
+    // ---- x -> exact split planes [16 px][cinp] (pixels past P and channels past Cin: zero)
+    for (int u = tid; u < 16 * (cinp / 8); u += kIrThreads) {
+        const int px = u / (cinp / 8), oc = u - px * (cinp / 8);
+        const int img = px / HW, p = px - img * HW;
+        const bool ok = px < P && n0 + img < a.N;
+        uint32_t b[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = 8 * oc + e;
+            b[e] = (ok && c < a.Cin) ? __float_as_uint(x[((int64_t)(n0 + img) * a.Cin + c) * HW + p]) : 0u;
+        }
+        uint4 hi, mid, lo;
+        split3(b, hi, mid, lo);
+        const int off = px * cinp * 2 + 16 * oc;
+        *reinterpret_cast<uint4*>(xpl + off) = hi;
+        *reinterpret_cast<uint4*>(xpl + xplane + off) = mid;
+        *reinterpret_cast<uint4*>(xpl + 2 * xplane + off) = lo;
+    }
+    const float se = *a.we_scale, sp = *a.wp_scale;
+    const int tg = wave % TG, sw = wave / TG, nsw = kIrWaves / TG;
+    const int nslices = a.Ch / 32;
+
+    // ---- register-held operands of a slice
+    uint4 bwe[kIrKse][2];
+    float e1s[2], e1b[2];
+    auto load_e = [&](int sl) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int tile = 2 * sl + t;
+#pragma unroll
+            for (int ks = 0; ks < kIrKse; ++ks)
+                bwe[ks][t] = ks < a.KSe ? a.we[((int64_t)ks * a.NTe + tile) * 64 + lane] : z4;
+            e1s[t] = a.ps1 ? a.ps1[16 * tile + pl] : 1.0f;
+            e1b[t] = a.pb1 ? a.pb1[16 * tile + pl] : 0.0f;
+        }
+    };
+    float dwv[11];  // the depthwise taps, bn2 scale and shift of this lane's channel
+    const int dc = lane & 31, dh = lane >> 5;
+    auto load_d = [&](int sl) __attribute__((always_inline)) {
+        const int h = 32 * sl + dc;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) dwv[k] = a.wd[h * 9 + k];
+        dwv[9] = a.ps2 ? a.ps2[h] : 1.0f;
+        dwv[10] = a.pb2 ? a.pb2[h] : 0.0f;
+    };
+    uint4 bwp[NTW];
+    auto load_p = [&](int sl) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            const int ot = tg * NTW + i;
+            bwp[i] = ot < a.NTp ? a.wp[((int64_t)sl * a.NTp + ot) * 64 + lane] : z4;
+        }
+    };
+    floatx4 acc[NTW];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (sw < nslices) {
+        load_e(sw);
+        load_d(sw);
+        load_p(sw);
+    }
+    lds_barrier();  // x planes
+
+    for (int sl = sw; sl < nslices; sl += nsw) {
+        const bool more = sl + nsw < nslices;
+        // ---- expand: this slice's two hidden tiles
+        floatx4 c[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < kIrKse; ++ks) {
+            if (ks >= a.KSe) break;
+            const int off = pl * cinp * 2 + 16 * (4 * ks + g);
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xpl + off));
+            const bf16x8 am = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xpl + xplane + off));
+            const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xpl + 2 * xplane + off));
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const bf16x8 bw = __builtin_bit_cast(bf16x8, bwe[ks][t]);
+                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, c[t], 0, 0, 0);
+                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, c[t], 0, 0, 0);
+                c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, c[t], 0, 0, 0);
+            }
+        }
+        // lane: hidden channel 16 t + pl of the slice, pixels 4 g .. 4 g + 3 (conv_pw's epilogue)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            floatx4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float q = c[t][e] * se + 0.0f;
+                q = q * e1s[t] + e1b[t];
+                v[e] = epi_act(q, a.act1);
+            }
+            *reinterpret_cast<floatx4*>(hidw + (16 * t + pl) * 16 + 4 * g) = v;
+        }
+        if (more) load_e(sl + nsw);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own hidden writes
+        // ---- depthwise: lane = channel dc of the slice, output pixels dh, dh + 2, .. (<= 16)
+#pragma unroll 2
+        for (int k8 = 0; k8 < 8; ++k8) {
+            const int op = dh + 2 * k8;
+            const int img = op / HWo, r = op - img * HWo;
+            const int oy = r / a.Wo, ox = r - oy * a.Wo;
+            const bool ok = op < Po && n0 + img < a.N;
+            const int imc = min(img, a.G - 1);
+            float hv[9];
+            bool tin[9];
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const int iy = oy * a.S - 1 + rr;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int ix = ox * a.S - 1 + t;
+                    tin[rr * 3 + t] = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                    const int pix = imc * HW + min(max(iy, 0), a.H - 1) * a.W + min(max(ix, 0), a.W - 1);
+                    hv[rr * 3 + t] = hidw[dc * 16 + pix];
+                }
+            }
+            float s = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) s = fmaf(tin[k] ? hv[k] : 0.0f, dwv[k], s);
+            float q = s + 0.0f;  // conv_dw3's epilogue
+            q = q * dwv[9] + dwv[10];
+            const float v = ok ? epi_act(q, a.act2) : 0.0f;
+            uint16_t h16, m16, l16;
+            split1(__float_as_uint(v), h16, m16, l16);
+            const int off = op * 64 + dc * 2;
+            *reinterpret_cast<uint16_t*>(dplw + off) = h16;
+            *reinterpret_cast<uint16_t*>(dplw + 1024 + off) = m16;
+            *reinterpret_cast<uint16_t*>(dplw + 2048 + off) = l16;
+        }
+        if (more) load_d(sl + nsw);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own d-plane writes
+        // ---- project: the slice's k-step into this wave's output tiles
+        {
+            const int off = pl * 64 + 16 * g;
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(dplw + off));
+            const bf16x8 am = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(dplw + 1024 + off));
+            const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(dplw + 2048 + off));
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) {
+                if (tg * NTW + i >= a.NTp) break;  // wave-uniform
+                const bf16x8 bw = __builtin_bit_cast(bf16x8, bwp[i]);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, acc[i], 0, 0, 0);
+            }
+        }
+        if (more) load_p(sl + nsw);
+    }
+
+    // ---- the waves' partial sums meet in LDS (aliasing the planes: every wave is past them)
+    lds_barrier();
+    floatx4* red = reinterpret_cast<floatx4*>(lds);
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) red[(wave * NTW + i) * 64 + lane] = acc[i];
+    lds_barrier();
+    // output tile ft (group ft / NTW, local tile ft % NTW): the sum over that group's waves in wave
+    // order; lane: output channel 16 ft + pl, pixels 4 g .. 4 g + 3
+    for (int ft = wave; ft < a.NTp; ft += kIrWaves) {
+        const int grp = ft / NTW, i = ft - grp * NTW;
+        floatx4 v = red[(grp * NTW + i) * 64 + lane];
+        for (int w = grp + TG; w < kIrWaves; w += TG) v += red[(w * NTW + i) * 64 + lane];
+        const int k = 16 * ft + pl;
+        if (k >= a.Cout) continue;
+        const float s3 = a.ps3 ? a.ps3[k] : 1.0f, b3 = a.pb3 ? a.pb3[k] : 0.0f;
+        int yi[4];
+        float rv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int op = 4 * g + e;
+            const int img = op / HWo, r = op - img * HWo;
+            const bool ok = op < Po && n0 + img < a.N;
+            yi[e] = ok ? ((n0 + img) * a.Cout + k) * HWo + r : -1;
+            rv[e] = (ok && a.res) ? a.res[yi[e]] : 0.0f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float q = v[e] * sp + 0.0f;
+            q = q * s3 + b3;
+            if (a.res) q += rv[e];
+            if (yi[e] >= 0) y[yi[e]] = epi_act(q, a.act3);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ planning --
 namespace {
 
@@ -454,6 +674,37 @@ bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t C
     if (N * Cin * H * W >= INT32_MAX || N * Cout * H * W >= INT32_MAX || N * Ch * H * W >= ((int64_t)1 << 40))
         return false;
     const int64_t Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+    const int64_t NTp = (Cout + 15) / 16;
+    // small images: the slice-per-wave kernel (PO2Q_IR_SMALL=0: off, A/B)
+    const char* sm = getenv("PO2Q_IR_SMALL");
+    if (expand && H * W <= 16 && Ch % 32 == 0 && Cin <= 32 * kIrKse && NTp <= 24 && !(sm && sm[0] == '0')) {
+        IrPlan q{};
+        int64_t G = 1;
+        while (G * 2 * H * W <= 16 && G * 2 <= N) G *= 2;  // one 16-pixel tile of G images
+        q.small = 1;
+        q.tg = NTp <= 12 ? 1 : 2;
+        const int64_t per = (NTp + q.tg - 1) / q.tg;
+        q.ntw = per <= 4 ? 4 : (per <= 8 ? 8 : 12);
+        q.G = (int)G;
+        q.R = (int)Ho;
+        q.RI = (int)H;
+        q.nbands = 1;
+        q.CHK = 32;
+        q.P = (int)(G * H * W);
+        q.Po = 16;
+        const size_t xb = (size_t)3 * 16 * (32 * ((Cin + 31) / 32)) * 2;
+        q.lds = std::max(xb + (size_t)kIrWaves * kIrsWave, (size_t)kIrWaves * q.ntw * 1024);
+        q.blocks = (N + G - 1) / G;
+        ip = q;
+        return true;
+    }
+    // The chunked kernel for larger images is opt-in (PO2Q_IR_LARGE=1): at the sizes measured it
+    // ties or loses to the three layer launches replayed from a HIP graph (profiles/r04_ir_ab.jsonl),
+    // so by default those blocks run as the layers (po2q_qconv2d_ir_supported says 0).
+    {
+        const char* lg = getenv("PO2Q_IR_LARGE");
+        if (!(lg && lg[0] == '1')) return false;
+    }
     IrPlan q{};
     bool found = false;
     int64_t R = Ho, G = 1;
@@ -536,6 +787,23 @@ hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int
         hipLaunchKernelGGL(kern, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a);
         return hipGetLastError();
     };
+    if (ip.small) {
+        auto gs = [&](auto kern) -> hipError_t {
+            if (ip.lds > 64 * 1024) {
+                const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kIrLds);
+                if (attr != hipSuccess) return attr;
+            }
+            hipLaunchKernelGGL(kern, dim3((unsigned)ip.blocks), dim3(kIrThreads), ip.lds, s, x, y, a, ip.tg);
+            return hipGetLastError();
+        };
+        switch (ip.ntw) {
+            case 4: return gs(conv_ir_small<4>);
+            case 8: return gs(conv_ir_small<8>);
+            case 12: return gs(conv_ir_small<12>);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (ip.CHK) {
         case 32: return go(conv_ir<1>);
         case 64: return go(conv_ir<2>);

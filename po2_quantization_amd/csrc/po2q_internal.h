@@ -197,6 +197,8 @@ struct IrPlan {
     int G, R, RI, nbands, CHK, P, PG, Po, HP, xs;
     size_t lds, off_hid, off_dpl, off_cw;
     int64_t blocks;
+    int small = 0;     // 1: conv_ir_small (G images of <= 16 pixels in one MFMA tile, hidden slices per wave)
+    int ntw = 0, tg = 0;  // small: output tiles per wave, wave groups over the output tiles
 };
 struct IrEpi {
     const float *ps1, *pb1, *ps2, *pb2, *ps3, *pb3;  // each optional (NULL)

@@ -92,9 +92,17 @@ SHAPES = [(3, 32, 32, 16, 16, 16, 1, False), (3, 16, 96, 24, 16, 16, 2, True), (
           (2, 20, 40, 20, 11, 6, 1, True)]
 
 
+# kernel selection: "default" = the small-image kernel where it applies (<= 16 pixels per image),
+# the layer launches elsewhere; "chunked" = the chunked kernel for every shape (opt-in knobs)
+KERNELS = {"default": {}, "chunked": {"PO2Q_IR_LARGE": "1", "PO2Q_IR_SMALL": "0"}}
+
+
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 @pytest.mark.parametrize("mode,bits", [("po2", 4), ("po2+", 3)])
-def test_ir_block_vs_torch_and_layers(shape, mode, bits):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_ir_block_vs_torch_and_layers(shape, mode, bits, kernel, monkeypatch):
+    for k, v in KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     N, Cin, Ch, Cout, H, W, s, expand = shape
     x, we, wd, wp, bn = make_block(N, Cin, Ch, Cout, H, W, hash(shape) & 0xFFFF, expand)
     res = x if (s == 1 and Cin == Cout) else None
@@ -108,12 +116,32 @@ def test_ir_block_vs_torch_and_layers(shape, mode, bits):
 
 
 @pytest.mark.parametrize("acts", [("silu", "silu", "none"), ("relu", "relu6", "relu"), ("none", "none", "silu")])
-def test_ir_block_activations(acts):
-    """MobileViT's MV2Block uses SiLU (mobile_vit.py:131-239); every activation at every position."""
-    x, we, wd, wp, bn = make_block(4, 16, 64, 16, 8, 8, 7)
+@pytest.mark.parametrize("hw", [8, 2])
+def test_ir_block_activations(acts, hw, monkeypatch):
+    """MobileViT's MV2Block uses SiLU (mobile_vit.py:131-239); every activation at every position,
+    in the chunked (8x8) and the small-image (2x2) kernel."""
+    monkeypatch.setenv("PO2Q_IR_LARGE", "1")
+    x, we, wd, wp, bn = make_block(4, 16, 64, 16, hw, hw, 7)
     y = run_ir(x, we, wd, wp, bn, 1, acts, x, "po2+", 4)
     ref = torch_block(x, we, wd, wp, bn, 1, acts, x, "po2+", 4)
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+
+
+@pytest.mark.parametrize("shape", [(40, 64, 384, 96, 2, 2, 1), (33, 160, 960, 320, 1, 1, 1), (17, 32, 192, 64, 4, 4, 2),
+                                   (9, 24, 96, 24, 3, 3, 1), (5, 96, 576, 160, 2, 2, 2), (3, 16, 64, 200, 1, 1, 1)],
+                         ids=str)
+def test_ir_small_kernel_groups(shape):
+    """The small-image kernel: G images per block (16 at 1x1, 4 at 2x2, 1 from 3x3), partial last
+    groups, two output-tile wave groups (Cout > 192), stride 2, a 3x3 image (9 of 16 tile rows)."""
+    N, Cin, Ch, Cout, H, W, s = shape
+    x, we, wd, wp, bn = make_block(N, Cin, Ch, Cout, H, W, N + Ch)
+    res = x if (s == 1 and Cin == Cout) else None
+    acts = ("relu6", "relu6", "none")
+    y = run_ir(x, we, wd, wp, bn, s, acts, res, "po2", 4)
+    ref = torch_block(x, we, wd, wp, bn, s, acts, res, "po2", 4)
+    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+    lay = layer_chain(x, we, wd, wp, bn, s, acts, res, "po2", 4)
+    assert nerr(y, lay) <= CONV_TOL, nerr(y, lay)
 
 
 def test_ir_unsupported_shape_runs_the_layers():
@@ -146,9 +174,11 @@ def _plan(L, N, C, H, W, K, R, S, st, pad, groups, bits, mode):
     return h
 
 
-def test_ir_through_the_c_abi():
+def test_ir_through_the_c_abi(monkeypatch):
     """The C ABI as a non-torch binding uses it: plan handles, po2q_qconv2d_plan_pack_batch, then
-    po2q_qconv2d_ir_supported / po2q_qconv2d_ir_f32 on the current stream."""
+    po2q_qconv2d_ir_supported / po2q_qconv2d_ir_f32 on the current stream (8x8: the chunked kernel,
+    opt-in)."""
+    monkeypatch.setenv("PO2Q_IR_LARGE", "1")
     L = _lib.load()
     N, Cin, Ch, Cout, H, s = 4, 24, 144, 24, 8, 1
     x, we, wd, wp, bn = make_block(N, Cin, Ch, Cout, H, H, 21)

@@ -48,8 +48,10 @@ def main():
     ap.add_argument("--only-fused", action="store_true")
     ap.add_argument("--no-ir", action="store_true",
                     help="inverted-residual blocks as three fused layer calls instead of one block launch")
+    ap.add_argument("--ir", action="store_true", help="inverted-residual blocks as one launch where it applies")
     args = ap.parse_args()
-    quantized_conv.IR_FUSION = not args.no_ir
+    if args.ir or args.no_ir:
+        quantized_conv.IR_FUSION = bool(args.ir)
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
     m = get_model(args.model, args.classes, quantizer_dict[args.quantizer], args.bits,
