@@ -677,7 +677,12 @@ bool ir_plan(IrPlan& ip, int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t C
     const int64_t NTp = (Cout + 15) / 16;
     // small images: the slice-per-wave kernel (PO2Q_IR_SMALL=0: off, A/B)
     const char* sm = getenv("PO2Q_IR_SMALL");
-    if (expand && H * W <= 16 && Ch % 32 == 0 && Cin <= 32 * kIrKse && NTp <= 24 && !(sm && sm[0] == '0')) {
+    // Default only for images of 9..16 pixels (one image per block): 18 vs 25 us per block at 4x4 bs 256,
+    // where at 2x2 / 1x1 (several images per block, each block streaming all the weights) it loses to
+    // the layer launches (profiles/r04_ir_small_ab.jsonl); PO2Q_IR_SMALL=1 takes every size <= 16.
+    const bool small_all = sm && sm[0] == '1';
+    if (expand && H * W <= 16 && (H * W >= 9 || small_all) && Ch % 32 == 0 && Cin <= 32 * kIrKse && NTp <= 24 &&
+        !(sm && sm[0] == '0')) {
         IrPlan q{};
         int64_t G = 1;
         while (G * 2 * H * W <= 16 && G * 2 <= N) G *= 2;  // one 16-pixel tile of G images

@@ -357,11 +357,12 @@ def run_fused_sequence(seq, x, residual=None):
 
 # Whole inverted-residual blocks (mobilenet.py:53-134, mobile_vit.py:131-239) as ONE launch
 # (torch.ops.po2q.qconv2d_ir: expand -> depthwise -> project with the hidden activations on
-# chip) inside a batched_packs forward, from the three layers' batched packs.  Off by default:
-# at CIFAR size the block kernel is latency-bound in its hidden-channel chunk loop and loses to
-# the three fused layer launches replayed from a HIP graph on 8 of the 12 MobileNetV2 @32 block
-# shapes (profiles/r04_ir_ab.jsonl: 24-120 us against 20-42 us per block); True for A/B runs.
-IR_FUSION = False
+# chip) inside a batched_packs forward, from the three layers' batched packs.  The op fuses only
+# where the block kernel measured faster than the three fused layer launches replayed from a HIP
+# graph -- the small-image kernel at 3x3 / 4x4 (po2q_qconv2d_ir_supported; profiles/r04_ir_ab.jsonl,
+# r04_ir_small_ab.jsonl) -- and runs the layers from the same packs elsewhere.  False: always the
+# layer calls (A/B runs).
+IR_FUSION = True
 
 
 def _ir_spec(seq):

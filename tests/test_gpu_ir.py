@@ -92,9 +92,10 @@ SHAPES = [(3, 32, 32, 16, 16, 16, 1, False), (3, 16, 96, 24, 16, 16, 2, True), (
           (2, 20, 40, 20, 11, 6, 1, True)]
 
 
-# kernel selection: "default" = the small-image kernel where it applies (<= 16 pixels per image),
-# the layer launches elsewhere; "chunked" = the chunked kernel for every shape (opt-in knobs)
-KERNELS = {"default": {}, "chunked": {"PO2Q_IR_LARGE": "1", "PO2Q_IR_SMALL": "0"}}
+# kernel selection: "default" = the small-image kernel for 3x3 / 4x4 images, the layer launches
+# elsewhere; "small" = the small-image kernel for every image <= 16 pixels; "chunked" = the chunked
+# kernel for every shape (opt-in knobs)
+KERNELS = {"default": {}, "small": {"PO2Q_IR_SMALL": "1"}, "chunked": {"PO2Q_IR_LARGE": "1", "PO2Q_IR_SMALL": "0"}}
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
@@ -130,9 +131,11 @@ def test_ir_block_activations(acts, hw, monkeypatch):
 @pytest.mark.parametrize("shape", [(40, 64, 384, 96, 2, 2, 1), (33, 160, 960, 320, 1, 1, 1), (17, 32, 192, 64, 4, 4, 2),
                                    (9, 24, 96, 24, 3, 3, 1), (5, 96, 576, 160, 2, 2, 2), (3, 16, 64, 200, 1, 1, 1)],
                          ids=str)
-def test_ir_small_kernel_groups(shape):
-    """The small-image kernel: G images per block (16 at 1x1, 4 at 2x2, 1 from 3x3), partial last
-    groups, two output-tile wave groups (Cout > 192), stride 2, a 3x3 image (9 of 16 tile rows)."""
+def test_ir_small_kernel_groups(shape, monkeypatch):
+    """The small-image kernel: G images per block (16 at 1x1, 4 at 2x2, 1 from 3x3; below 3x3 opt-in),
+    partial last groups, two output-tile wave groups (Cout > 192), stride 2, a 3x3 image (9 of 16 tile
+    rows)."""
+    monkeypatch.setenv("PO2Q_IR_SMALL", "1")
     N, Cin, Ch, Cout, H, W, s = shape
     x, we, wd, wp, bn = make_block(N, Cin, Ch, Cout, H, W, N + Ch)
     res = x if (s == 1 and Cin == Cout) else None

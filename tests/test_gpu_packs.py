@@ -55,7 +55,9 @@ def test_packed_run_checks_workspace():
                                                ("mobilevit", 64, "po2+", 2)])
 def test_model_forward_batched_packs_bit_exact(name, image, q, bits, monkeypatch):
     """The models' eval forwards: the first forward at a shape records the layers, later forwards pack
-    them in batched launches up front; logits bit for bit those of the per-layer packs."""
+    them in batched launches up front; logits bit for bit those of the per-layer packs (the fused
+    inverted-residual block, which sums in another order, is off here: tests/test_gpu_ir.py)."""
+    monkeypatch.setattr(qc, "IR_FUSION", False)
     torch.manual_seed(0)
     m = get_model(name, 10, quantizer_dict[q], bits, (image, image)).to(DEV).eval()
     x = torch.randn(4, 3, image, image, device=DEV)
