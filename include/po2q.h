@@ -378,9 +378,15 @@ int po2q_qconv2d_plan_run_packed(const po2q_conv_plan* plan, const float* x, con
  * fp32 FMAs -- the layer chain's result up to the pointwise k-split summation order.
  * po2q_qconv2d_ir_supported: 1 when the three plans chain and a block geometry fits, 0 when not
  * (po2q_last_error() says why; run the three layers instead), < 0 on a bad argument.
+ * po2q_qconv2d_ir_shape_supported: the same geometry test from the shapes alone (before any plan
+ * exists): 1 when the block kernel takes it by default -- the small-image kernel at 3x3 / 4x4 images
+ * (PO2Q_IR_SMALL=1: every image of <= 16 pixels; PO2Q_IR_LARGE=1: the chunked kernel for larger
+ * ones), where it measured faster than the three layer launches.
  */
 int po2q_qconv2d_ir_supported(const po2q_conv_plan* expand, const po2q_conv_plan* depthwise,
                               const po2q_conv_plan* project);
+int po2q_qconv2d_ir_shape_supported(int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout,
+                                    int64_t stride, int expand);
 int po2q_qconv2d_ir_f32(const float* x, float* y, const po2q_conv_plan* expand, const void* ws_e, size_t ws_e_bytes,
                         const po2q_conv_plan* depthwise, const void* ws_d, size_t ws_d_bytes,
                         const po2q_conv_plan* project, const void* ws_p, size_t ws_p_bytes, const float* ps1,

@@ -65,6 +65,7 @@ EXPORTS = (
     "po2q_qconv2d_chain_workspace_bytes",
     "po2q_qconv2d_chain_f32",
     "po2q_qconv2d_ir_supported",
+    "po2q_qconv2d_ir_shape_supported",
     "po2q_qconv2d_ir_f32",
 )
 
@@ -171,6 +172,8 @@ def load():
     L.po2q_qconv2d_plan_packs_weight.argtypes = [p]
     L.po2q_qconv2d_ir_supported.restype = i32
     L.po2q_qconv2d_ir_supported.argtypes = [p, p, p]
+    L.po2q_qconv2d_ir_shape_supported.restype = i32
+    L.po2q_qconv2d_ir_shape_supported.argtypes = [i64] * 7 + [i32]
     L.po2q_qconv2d_ir_f32.restype = i32
     L.po2q_qconv2d_ir_f32.argtypes = [p, p, p, p, sz, p, p, sz, p, p, sz, p, p, i32, p, p, i32, p, p, p, i32, p]
     L.po2q_qconv2d_chain_supported.restype = i32
@@ -612,6 +615,13 @@ def qconv2d_packed(x, w, workspace, bias=None, stride=1, padding=0, dilation=1, 
     return _op_call(O.qconv2d_packed, xc, wc, workspace, bc, list(args[7:9]), list(args[9:11]), list(args[11:13]),
                     args[13], int(bits), MODES[mode], int(fsr), PRECISIONS[precision], -1 if saved is None else int(saved),
                     post_scale, post_shift, residual, ACTS[act])
+
+
+def ir_shape_supported(x_shape, Ch, Cout, stride, expand):
+    """Whether the fused inverted-residual kernel takes this block by default (po2q_qconv2d_ir_shape_supported:
+    where it measured faster than the three layer launches).  Host-only."""
+    N, Cin, H, W = (int(v) for v in x_shape)
+    return load().po2q_qconv2d_ir_shape_supported(N, Cin, H, W, int(Ch), int(Cout), int(stride), int(bool(expand))) == 1
 
 
 def qconv2d_ir(x, we, wd, wp, ws_e, ws_d, ws_p, stride=1, bits=4, mode="po2", fsr=1, precision="auto",

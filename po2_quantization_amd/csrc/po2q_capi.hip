@@ -717,6 +717,12 @@ static int ir_check(const po2q_conv_plan* e, const po2q_conv_plan* d, const po2q
     return PO2Q_OK;
 }
 
+int po2q_qconv2d_ir_shape_supported(int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Ch, int64_t Cout,
+                                    int64_t stride, int expand) {
+    po2q::IrPlan ip;
+    return po2q::ir_plan(ip, N, Cin, H, W, Ch, Cout, stride, expand != 0) ? 1 : 0;
+}
+
 int po2q_qconv2d_ir_supported(const po2q_conv_plan* expand, const po2q_conv_plan* depthwise,
                               const po2q_conv_plan* project) {
     po2q::IrPlan ip;

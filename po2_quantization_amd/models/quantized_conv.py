@@ -406,6 +406,11 @@ def run_inverted_residual(seq, x, residual=None):
     (which record the layers for the next forward's packs)."""
     sess = _packs
     spec = _ir_spec(seq) if IR_FUSION and sess is not None else None
+    if spec is not None and x.dim() == 4:  # only blocks the kernel takes: the others keep their tuned plans
+        d = spec[1][0]
+        if not _lib.ir_shape_supported(x.shape, d.out_channels, spec[2][0].out_channels, d.stride[0],
+                                       spec[0] is not None):
+            spec = None
     if spec is not None and sess.recording is not None:
         # record the block's layers with their heuristic plans (candidate 0: the pointwise and
         # depthwise kernels whose packs the block kernel reads), whatever the autotuner picked
