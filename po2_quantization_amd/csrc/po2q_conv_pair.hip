@@ -376,11 +376,16 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             for (int grp = 0; grp < NG; ++grp) {
                 const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
                 floatx4 v;
+                if constexpr (E == 0 || E == 2) {  // one fma per value, as packed v_pk_fma_f32 pairs
+                    const float sm = E == 0 ? scale2 : e2s[nt], ad = E == 0 ? 0.0f : e2b[nt];  // E 2: folded
+                    const po2q_float2 s2 = {sm, sm}, b2 = {ad, ad};
+                    const po2q_float2 v01 = po2q_float2{acc2[D][grp][nt][0], acc2[D][grp][nt][1]} * s2 + b2;
+                    const po2q_float2 v23 = po2q_float2{acc2[D][grp][nt][2], acc2[D][grp][nt][3]} * s2 + b2;
+                    v = floatx4{v01.x, v01.y, v23.x, v23.y};
+                } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
-                           : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
-                                    : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                    for (int e = 0; e < 4; ++e) v[e] = (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                }
                 if constexpr (RES) {
                     const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * (a.Wp * 4) + ql * 4)
                                          : *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
@@ -517,36 +522,40 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     uint32_t b4[4];
+                    if constexpr (E == 0) {  // packed v_pk_fma_f32 pairs (the same fma per value)
+                        const po2q_float2 s1 = {scale1, scale1}, z = {0.0f, 0.0f};
+                        const po2q_float2 t01 = po2q_float2{acc1[D][grp][nt][0], acc1[D][grp][nt][1]} * s1 + z;
+                        const po2q_float2 t23 = po2q_float2{acc1[D][grp][nt][2], acc1[D][grp][nt][3]} * s1 + z;
+                        b4[0] = __float_as_uint(t01.x);
+                        b4[1] = __float_as_uint(t01.y);
+                        b4[2] = __float_as_uint(t23.x);
+                        b4[3] = __float_as_uint(t23.y);
+                    } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float t;
-                        if constexpr (E == 0) {
-                            t = acc1[D][grp][nt][e] * scale1 + 0.0f;
-                        } else if constexpr (E == 2) {
-                            const int c = nt * 4 + e;
-                            t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
-                            t = t < 0.0f ? 0.0f : t;
-                        } else {
-                            const int c = nt * 4 + e;
-                            t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
+                        for (int e = 0; e < 4; ++e) {
+                            float t;
+                            if constexpr (E == 2) {
+                                const int c = nt * 4 + e;
+                                t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
+                                t = t < 0.0f ? 0.0f : t;
+                            } else {
+                                const int c = nt * 4 + e;
+                                t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
+                            }
+                            b4[e] = __float_as_uint(t);
                         }
-                        b4[e] = __float_as_uint(t);
                     }
                     if (!allok) {  // wave-uniform: only rows / strips that leave the image pay the select
                         const bool ok = irow && q < a.W;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) b4[e] = ok ? b4[e] : 0u;
                     }
-                    uint16_t h[4], m[4], l[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
+                    uint2 h2, m2, l2;
+                    split4p(b4, h2, m2, l2);
                     const int wo = yoct<CC>(q + 1, (4 * nt + g) >> 1) + 8 * (g & 1);
-                    *reinterpret_cast<uint2*>(yw + wo) =
-                        make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-                    *reinterpret_cast<uint2*>(yw + YPL + wo) =
-                        make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
-                    *reinterpret_cast<uint2*>(yw + 2 * YPL + wo) =
-                        make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+                    *reinterpret_cast<uint2*>(yw + wo) = h2;
+                    *reinterpret_cast<uint2*>(yw + YPL + wo) = m2;
+                    *reinterpret_cast<uint2*>(yw + 2 * YPL + wo) = l2;
                 }
             }
         }

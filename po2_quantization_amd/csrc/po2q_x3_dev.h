@@ -38,22 +38,57 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // (a >> 16) | (b & 0xffff0000): the bf16 halves of a (low) and b (high) as one dword
 __device__ __forceinline__ uint32_t pk_hi16(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
 
+typedef float po2q_float2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
     uint32_t mb[8], lb[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; j += 2) {
         // +-inf: r1 from the value clamped to +-FLT_MAX (one v_med3 instead of a class test and
-        // a select): finite mid / lo beside hi = +-inf, so every product sum stays +-inf
-        const float xc = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
-        const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
-        mb[j] = __float_as_uint(r1) & 0xffff0000u;
-        lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
+        // a select): finite mid / lo beside hi = +-inf, so every product sum stays +-inf.  The two
+        // subtractions of a value pair are one packed v_pk_add_f32 each (same IEEE results).
+        const float xc0 = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
+        const float xc1 = __builtin_amdgcn_fmed3f(__uint_as_float(b[j + 1]), -3.40282347e38f, 3.40282347e38f);
+        const po2q_float2 xc = {xc0, xc1};
+        const po2q_float2 h = {__uint_as_float(__float_as_uint(xc0) & 0xffff0000u),
+                               __uint_as_float(__float_as_uint(xc1) & 0xffff0000u)};
+        const po2q_float2 r1 = xc - h;
+        mb[j] = __float_as_uint(r1.x) & 0xffff0000u;
+        mb[j + 1] = __float_as_uint(r1.y) & 0xffff0000u;
+        const po2q_float2 m = {__uint_as_float(mb[j]), __uint_as_float(mb[j + 1])};
+        const po2q_float2 l = r1 - m;
+        lb[j] = __float_as_uint(l.x);
+        lb[j + 1] = __float_as_uint(l.y);
     }
     // the upper halves of two dwords in one v_perm_b32 (the shift + and_or pair it replaces
     // cost two vector instructions per packed dword)
     hi = make_uint4(pk_hi16(b[0], b[1]), pk_hi16(b[2], b[3]), pk_hi16(b[4], b[5]), pk_hi16(b[6], b[7]));
     mid = make_uint4(pk_hi16(mb[0], mb[1]), pk_hi16(mb[2], mb[3]), pk_hi16(mb[4], mb[5]), pk_hi16(mb[6], mb[7]));
     lo = make_uint4(pk_hi16(lb[0], lb[1]), pk_hi16(lb[2], lb[3]), pk_hi16(lb[4], lb[5]), pk_hi16(lb[6], lb[7]));
+}
+
+// The same for 4 values (the epilogues' 4 channels of one pixel): 4 bf16 per plane, packed in
+// channel order (low half = the even channel).
+__device__ __forceinline__ void split4p(const uint32_t (&b)[4], uint2& hi, uint2& mid, uint2& lo) {
+    uint32_t mb[4], lb[4];
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+        const float xc0 = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
+        const float xc1 = __builtin_amdgcn_fmed3f(__uint_as_float(b[j + 1]), -3.40282347e38f, 3.40282347e38f);
+        const po2q_float2 xc = {xc0, xc1};
+        const po2q_float2 h = {__uint_as_float(__float_as_uint(xc0) & 0xffff0000u),
+                               __uint_as_float(__float_as_uint(xc1) & 0xffff0000u)};
+        const po2q_float2 r1 = xc - h;
+        mb[j] = __float_as_uint(r1.x) & 0xffff0000u;
+        mb[j + 1] = __float_as_uint(r1.y) & 0xffff0000u;
+        const po2q_float2 m = {__uint_as_float(mb[j]), __uint_as_float(mb[j + 1])};
+        const po2q_float2 l = r1 - m;
+        lb[j] = __float_as_uint(l.x);
+        lb[j + 1] = __float_as_uint(l.y);
+    }
+    hi = make_uint2(pk_hi16(b[0], b[1]), pk_hi16(b[2], b[3]));
+    mid = make_uint2(pk_hi16(mb[0], mb[1]), pk_hi16(mb[2], mb[3]));
+    lo = make_uint2(pk_hi16(lb[0], lb[1]), pk_hi16(lb[2], lb[3]));
 }
 
 // Epilogue stores as inline asm: hipcc then leaves them out of its vmcnt
