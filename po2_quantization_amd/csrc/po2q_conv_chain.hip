@@ -121,21 +121,6 @@ struct ChainArgs {
     } while (0)
 #endif
 
-// Exact 3-way split of 4 fp32 values (split3 of po2q_x3_dev.h, 4 lanes of it): 4 bf16 per plane.
-__device__ __forceinline__ void split4(const float (&v)[4], uint2& hi, uint2& mid, uint2& lo) {
-    uint32_t b[4], mb[4], lb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        b[j] = __float_as_uint(v[j]);
-        const float xc = __builtin_amdgcn_fmed3f(v[j], -3.40282347e38f, 3.40282347e38f);
-        const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
-        mb[j] = __float_as_uint(r1) & 0xffff0000u;
-        lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
-    }
-    hi = make_uint2((b[0] >> 16) | (b[1] & 0xffff0000u), (b[2] >> 16) | (b[3] & 0xffff0000u));
-    mid = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
-    lo = make_uint2((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u));
-}
 
 // C: channels; MG: most 16-pixel groups one wave owns (register arrays).  The activation lives
 // in LDS as split planes for the whole chain: per layer every wave first computes ALL its
@@ -410,11 +395,18 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             if (!FULL && (grp >= ngroups || f >= HW)) continue;
             float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float u = (acc[gi][i] * scale + cbk[i]) * ceps[i] + cepb[i];
-                if (res_add) u += rres[gi][i];
-                v[i] = epi_act(u, act);
-                if (keep) rres[gi][i] = v[i];
+            for (int i = 0; i < 4; i += 2) {  // channel pairs as packed v_pk_fma / v_pk_add (the same IEEE ops)
+                const po2q_float2 sc = {scale, scale};
+                po2q_float2 u = (po2q_float2{acc[gi][i], acc[gi][i + 1]} * sc + po2q_float2{cbk[i], cbk[i + 1]}) *
+                                    po2q_float2{ceps[i], ceps[i + 1]} +
+                                po2q_float2{cepb[i], cepb[i + 1]};
+                if (res_add) u += po2q_float2{rres[gi][i], rres[gi][i + 1]};
+                v[i] = epi_act(u.x, act);
+                v[i + 1] = epi_act(u.y, act);
+                if (keep) {
+                    rres[gi][i] = v[i];
+                    rres[gi][i + 1] = v[i + 1];
+                }
             }
             if (last) {
 #pragma unroll
@@ -423,7 +415,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 const int oy = f / W, ox = f - oy * W;
                 const int ad = ch_addr<C, W8, S16>((oy + 1) * PW + ox + 1, ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
                 uint2 hi, mid, lo;
-                split4(v, hi, mid, lo);
+                const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                        __float_as_uint(v[3])};
+                split4p(vb, hi, mid, lo);
                 *reinterpret_cast<uint2*>(lds + wr + ad) = hi;
                 *reinterpret_cast<uint2*>(lds + wr + a.PL + ad) = mid;
                 *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
