@@ -140,6 +140,14 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // its own x DMA of the previous step AND every store issued before it.  Plain / general forms
 // without a residual, seven compute waves (C = 16: 192 < W <= 224, C = 32: 96 < W <= 112); a row is
 // 14 DMA instructions either way (C x 7 * 512 / C / 4 float4).
+// Packed fp32 (v_pk_fma / v_pk_add) in this kernel's exact splits and plain epilogues: off by
+// default -- same IEEE results, fewer VALU instructions, but the kernel measured 2-4 % slower
+// with them (same-box A/B, profiles/r04_pair_packed_ab.jsonl); -DPO2Q_PAIR_PK=1 builds them.
+#ifndef PO2Q_PAIR_PK
+#define PO2Q_PAIR_PK 0
+#endif
+constexpr bool kPairPK = PO2Q_PAIR_PK != 0;
+
 template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0, int MW = 0>
 __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             for (int grp = 0; grp < NG; ++grp) {
                 const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
                 floatx4 v;
-                if constexpr (E == 0 || E == 2) {  // one fma per value, as packed v_pk_fma_f32 pairs
+                if constexpr ((E == 0 || E == 2) && kPairPK) {  // one fma per value, as packed v_pk_fma_f32 pairs
                     const float sm = E == 0 ? scale2 : e2s[nt], ad = E == 0 ? 0.0f : e2b[nt];  // E 2: folded
                     const po2q_float2 s2 = {sm, sm}, b2 = {ad, ad};
                     const po2q_float2 v01 = po2q_float2{acc2[D][grp][nt][0], acc2[D][grp][nt][1]} * s2 + b2;
@@ -384,7 +392,10 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                     v = floatx4{v01.x, v01.y, v23.x, v23.y};
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
+                               : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
+                                        : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
                 }
                 if constexpr (RES) {
                     const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * (a.Wp * 4) + ql * 4)
@@ -442,7 +453,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     auto split_x = [&](const uint32_t (&bx)[8], uint32_t hx) __attribute__((always_inline)) {
         if constexpr ((DBG & 16) != 0) return;
         uint4 hi, mid, lo;
-        split3(bx, hi, mid, lo);
+        split3<kPairPK>(bx, hi, mid, lo);
         *reinterpret_cast<uint4*>(slab + wa_i) = hi;
         *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
         *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
@@ -522,7 +533,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     uint32_t b4[4];
-                    if constexpr (E == 0) {  // packed v_pk_fma_f32 pairs (the same fma per value)
+                    if constexpr (E == 0 && kPairPK) {  // packed v_pk_fma_f32 pairs (the same fma per value)
                         const po2q_float2 s1 = {scale1, scale1}, z = {0.0f, 0.0f};
                         const po2q_float2 t01 = po2q_float2{acc1[D][grp][nt][0], acc1[D][grp][nt][1]} * s1 + z;
                         const po2q_float2 t23 = po2q_float2{acc1[D][grp][nt][2], acc1[D][grp][nt][3]} * s1 + z;
@@ -534,7 +545,9 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             float t;
-                            if constexpr (E == 2) {
+                            if constexpr (E == 0) {
+                                t = acc1[D][grp][nt][e] * scale1 + 0.0f;
+                            } else if constexpr (E == 2) {
                                 const int c = nt * 4 + e;
                                 t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
                                 t = t < 0.0f ? 0.0f : t;
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                         for (int e = 0; e < 4; ++e) b4[e] = ok ? b4[e] : 0u;
                     }
                     uint2 h2, m2, l2;
-                    split4p(b4, h2, m2, l2);
+                    split4p<kPairPK>(b4, h2, m2, l2);
                     const int wo = yoct<CC>(q + 1, (4 * nt + g) >> 1) + 8 * (g & 1);
                     *reinterpret_cast<uint2*>(yw + wo) = h2;
                     *reinterpret_cast<uint2*>(yw + YPL + wo) = m2;
@@ -963,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair_ab(const float* __restrict__
 #pragma unroll
             for (int so = 0; so < 2; ++so) {
                 uint4 hi, mid, lo;
-                split3(bx[so], hi, mid, lo);
+                split3<kPairPK>(bx[so], hi, mid, lo);
                 const int wa = xa<CC>(lane + 1, so);
                 *reinterpret_cast<uint4*>(slab + wa) = hi;
                 *reinterpret_cast<uint4*>(slab + PL + wa) = mid;

@@ -40,8 +40,21 @@ __device__ __forceinline__ uint32_t pk_hi16(uint32_t a, uint32_t b) { return __b
 
 typedef float po2q_float2 __attribute__((ext_vector_type(2)));
 
+// PK (default): the two subtractions of a value pair as one v_pk_add_f32 each; PK false: scalar
+// v_sub_f32 per value (same IEEE results either way -- the conv pair keeps the scalar form, which
+// measured faster there: its packed operands need register-pair moves)
+template <bool PK = true>
 __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4& mid, uint4& lo) {
     uint32_t mb[8], lb[8];
+    if constexpr (!PK) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float xc = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
+            const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
+            mb[j] = __float_as_uint(r1) & 0xffff0000u;
+            lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
         // +-inf: r1 from the value clamped to +-FLT_MAX (one v_med3 instead of a class test and
@@ -60,6 +73,7 @@ __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4&
         lb[j] = __float_as_uint(l.x);
         lb[j + 1] = __float_as_uint(l.y);
     }
+    }
     // the upper halves of two dwords in one v_perm_b32 (the shift + and_or pair it replaces
     // cost two vector instructions per packed dword)
     hi = make_uint4(pk_hi16(b[0], b[1]), pk_hi16(b[2], b[3]), pk_hi16(b[4], b[5]), pk_hi16(b[6], b[7]));
@@ -69,8 +83,18 @@ __device__ __forceinline__ void split3(const uint32_t (&b)[8], uint4& hi, uint4&
 
 // The same for 4 values (the epilogues' 4 channels of one pixel): 4 bf16 per plane, packed in
 // channel order (low half = the even channel).
+template <bool PK = true>
 __device__ __forceinline__ void split4p(const uint32_t (&b)[4], uint2& hi, uint2& mid, uint2& lo) {
     uint32_t mb[4], lb[4];
+    if constexpr (!PK) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float xc = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
+            const float r1 = xc - __uint_as_float(__float_as_uint(xc) & 0xffff0000u);
+            mb[j] = __float_as_uint(r1) & 0xffff0000u;
+            lb[j] = __float_as_uint(r1 - __uint_as_float(mb[j]));
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < 4; j += 2) {
         const float xc0 = __builtin_amdgcn_fmed3f(__uint_as_float(b[j]), -3.40282347e38f, 3.40282347e38f);
@@ -85,6 +109,7 @@ __device__ __forceinline__ void split4p(const uint32_t (&b)[4], uint2& hi, uint2
         const po2q_float2 l = r1 - m;
         lb[j] = __float_as_uint(l.x);
         lb[j + 1] = __float_as_uint(l.y);
+    }
     }
     hi = make_uint2(pk_hi16(b[0], b[1]), pk_hi16(b[2], b[3]));
     mid = make_uint2(pk_hi16(mb[0], mb[1]), pk_hi16(mb[2], mb[3]));
