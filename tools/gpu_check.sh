@@ -44,6 +44,8 @@ for s in $STEPS; do
                 run models_c4 300 python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
         profmb) run profmb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profmb -o run \
                   -- python tools/model_bench.py --model mobilenet --image 32 --classes 10 --quantizer po2+ --only-fused ;;
+        profvit) run profvit 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profvit -o run \
+                  -- python tools/model_bench.py --model mobilevit --image 256 --batch 64 --quantizer po2+ --bits 2 --only-fused --graph ;;
         profr56) run profr56 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profr56 -o run \
                   -- python tools/model_bench.py --model resnet56 --image 224 --only-fused ;;
         bwdtests) run bwdtests 600 python -u -m pytest tests/test_gpu_backward.py tests/test_qat.py -m gpu -x -q --timeout 300 --timeout-method thread
