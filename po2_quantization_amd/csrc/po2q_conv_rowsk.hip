@@ -162,12 +162,18 @@ __device__ __forceinline__ void loader_wave(const float* __restrict__ x, const R
 //     into a 2-slot ring next to the output tile; act after the add)
 // FP (plan field fp, not with LW): the block reduces max|w| and each wave quantizes +
 //     packs its own VGPR-resident B fragments (po2q_quant_dev.h wq_*): one launch per layer
+// PIPE (not with LW / RES / FP): the split runs one row ahead.  Step j's MFMAs read the planes of
+//     row j (split in step j - 1) while the wave splits row j + 1 into the other plane buffer,
+//     between its first k-step's MFMAs and the next fragment reads, and the step's one barrier
+//     moves to its end: the split's vector and LDS work issues beside the matrix work instead of
+//     in front of it, behind a barrier.  Same arithmetic, same outputs bit for bit.
 template <int C, int PD, bool TT, bool LW, bool EPI = false, int DBG = 0, int NTS = 0, bool RES = false,
-          bool FP = false>
+          bool FP = false, bool PIPE = false>
 __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 3) : 4) void conv_rowsk(const float* __restrict__ x, const uint4* __restrict__ wpk,
                                                           const float* __restrict__ scale_p,
                                                           const float* __restrict__ bias, float* __restrict__ y,
                                                           RowsKArgs a) {
+    static_assert(!PIPE || (!LW && !RES && !FP && DBG == 0), "pipelined split: plain MFMA-wave plans");
     constexpr int K = C;
     constexpr int NCH = C / 32;        // 32-channel chunks (k-steps per tap: one per chunk)
     constexpr int KSC = 3 * NCH;       // k-steps per tap row
@@ -352,6 +358,29 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         }
     };
 
+    // exact split of halo row rw (this wave's channels + halo values) into the planes at pb
+    auto split_row = [&](const unsigned char* rw, unsigned char* pb) __attribute__((always_inline)) {
+        uint32_t b8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b8[e] = *reinterpret_cast<const uint32_t*>(rw + rd0 + e * (kKSW * 4));
+        uint4 hi, mid, lo;
+        split3(b8, hi, mid, lo);
+        if (sl_ok) {
+            *reinterpret_cast<uint4*>(pb + wa_i) = hi;
+            *reinterpret_cast<uint4*>(pb + PL + wa_i) = mid;
+            *reinterpret_cast<uint4*>(pb + 2 * PL + wa_i) = lo;
+        }
+        if (lane < HPW) {
+            uint16_t h16, m16, l16;
+            // halo value hv = HPW * wave + lane: own DMA at [wave][lane], LW's at [hv]
+            const int hoff = LW ? 4 * (HPW * wave + lane) : wave * 256 + 4 * lane;
+            split1(*reinterpret_cast<const uint32_t*>(rw + RAWI + hoff), h16, m16, l16);
+            *reinterpret_cast<uint16_t*>(pb + wa_h) = h16;
+            *reinterpret_cast<uint16_t*>(pb + PL + wa_h) = m16;
+            *reinterpret_cast<uint16_t*>(pb + 2 * PL + wa_h) = l16;
+        }
+    };
+
     floatx4 acc[3][NGW];
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl)
@@ -364,44 +393,36 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         constexpr int B2 = S6 % 2;  // plane buffer
         constexpr int RS = S6 % PD; // raw slot
         unsigned char* pb = planes + B2 * 3 * PL;
-        const unsigned char* rw = raw + RS * RAWS;
-        if constexpr (LW) {
-            // (the loader published row j at the previous barrier)
+        [[maybe_unused]] const unsigned char* rw = raw + RS * RAWS;
+        if constexpr (LW || PIPE) {
+            // (LW: the loader published row j at the previous barrier; PIPE: row j was split in
+            // step j - 1)
         } else if constexpr (DBG & 64) {
             rows_wait<31>();
         } else {
             rows_wait<VMW>();  // this wave's DMAs of row j have landed
         }
-        if constexpr (!(DBG & 4)) {
-            uint32_t b8[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) b8[e] = *reinterpret_cast<const uint32_t*>(rw + rd0 + e * (kKSW * 4));
-            uint4 hi, mid, lo;
-            split3(b8, hi, mid, lo);
-            if (sl_ok) {
-                *reinterpret_cast<uint4*>(pb + wa_i) = hi;
-                *reinterpret_cast<uint4*>(pb + PL + wa_i) = mid;
-                *reinterpret_cast<uint4*>(pb + 2 * PL + wa_i) = lo;
-            }
-            if (lane < HPW) {
-                uint16_t h16, m16, l16;
-                // halo value hv = HPW * wave + lane: own DMA at [wave][lane], LW's at [hv]
-                const int hoff = LW ? 4 * (HPW * wave + lane) : wave * 256 + 4 * lane;
-                split1(*reinterpret_cast<const uint32_t*>(rw + RAWI + hoff), h16, m16, l16);
-                *reinterpret_cast<uint16_t*>(pb + wa_h) = h16;
-                *reinterpret_cast<uint16_t*>(pb + PL + wa_h) = m16;
-                *reinterpret_cast<uint16_t*>(pb + 2 * PL + wa_h) = l16;
+        if constexpr (!PIPE) {
+            if constexpr (!(DBG & 4)) split_row(rw, pb);
+            // publish the planes: LDS writes done, then the block barrier (no memory fence:
+            // the prefetches and stores in flight must not be waited for)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            // refill the raw slot this wave just split (its own data only)
+            if constexpr (!(DBG & 128) && !LW) {
+                load_res(j + 1);
+                load_row(std::integral_constant<int, RS>{}, j + PD);
             }
         }
-        // publish the planes: LDS writes done, then the block barrier (no memory fence:
-        // the prefetches and stores in flight must not be waited for)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        // refill the raw slot this wave just split (its own data only)
-        if constexpr (!(DBG & 128) && !LW) {
-            load_res(j + 1);
-            load_row(std::integral_constant<int, RS>{}, j + PD);
-        }
+        // PIPE: end of step -- publish row j + 1's planes and this step's output tile, then refill
+        // row j + 1's raw slot with row j + 1 + PD
+        auto fin = [&]() __attribute__((always_inline)) {
+            if constexpr (PIPE) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                load_row(std::integral_constant<int, (S6 + 1) % PD>{}, j + 1 + PD);
+            }
+        };
         // MFMAs: halo row j feeds output halo-index j+1 (r=0), j (r=1), j-1 (r=2)
         constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
         // tap row rr of halo row j lands on segment output row j - rr: the edge steps (j < 2 or
@@ -409,7 +430,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         // branch per step picks the guarded or the branch-free body: a test per tap row inside
         // the k-step loop split the MFMA stream into blocks the scheduler could not interleave
         // (26 branches and ~110 s_waitcnt per step in the loop's ISA).
-        auto mma = [&](auto G_) __attribute__((always_inline)) {
+        auto mma = [&](auto G_, auto&& after0) __attribute__((always_inline)) {
             constexpr bool G = decltype(G_)::value;
 #pragma unroll
             for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
@@ -430,12 +451,26 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                             acc[SL[rr]][grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr][ks],
                                                                                       acc[SL[rr]][grp], 0, 0, 0);
                 }
+                if (ks == 0) after0();
             }
         };
-        if (j >= 2 && j < rbe)
-            mma(std::false_type{});
-        else
-            mma(std::true_type{});
+        if constexpr (PIPE) {
+            // row j + 1 (raw slot (S6 + 1) % PD) into the other plane buffer, beside k-step 0's MFMAs
+            auto nxt = [&]() __attribute__((always_inline)) {
+                rows_wait<(PD - 1) * (DPW + 1 + NGW)>();  // this wave's DMAs of row j + 1 have landed
+                split_row(raw + ((S6 + 1) % PD) * RAWS, planes + (1 - B2) * 3 * PL);
+            };
+            if (j >= 2 && j < rbe)
+                mma(std::false_type{}, nxt);
+            else
+                mma(std::true_type{}, nxt);
+        } else {
+            auto none = []() __attribute__((always_inline)) {};
+            if (j >= 2 && j < rbe)
+                mma(std::false_type{}, none);
+            else
+                mma(std::true_type{}, none);
+        }
         // output halo-index j-1 (row p0 + j - 2) is complete
         constexpr int D = (S + 2) % 3;
         if constexpr (TT) {
@@ -457,6 +492,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                     *reinterpret_cast<floatx4*>(tw + kout * (kKSW * 4) + ((bi ^ (kout & 7)) << 4)) = v;
                 acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
+            fin();
             return;
         }
         const int o = p0 + j - 2;
@@ -473,6 +509,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             rows_store<(NTS & 1) != 0>(ry, (orow && q < a.Q && !(DBG & 16)) ? (yk + (uint32_t)q) * 4u : 0x7fffffffu, v);
             acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
+        fin();
     };
 
     {
@@ -489,6 +526,13 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
             pre(std::integral_constant<int, 0>{});
             pre(std::integral_constant<int, 1>{});
             if constexpr (PD >= 3) pre(std::integral_constant<int, 2>{});
+            if constexpr (PIPE) {
+                rows_wait<VMW>();  // row 0
+                split_row(raw, planes);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                load_row(std::integral_constant<int, 0>{}, PD);
+            }
         }
     }
     for (int j = 0; j < nrows; j += 6) {
@@ -640,6 +684,33 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
 #define PO2Q_RKN(c, d, e, v, tt, lw) \
     PO2Q_RKN1(c, d, e, v, tt, lw, 1) PO2Q_RKN1(c, d, e, v, tt, lw, 2) PO2Q_RKN1(c, d, e, v, tt, lw, 3)
 #define PO2Q_RK(c, d, e) PO2Q_RK1(c, d, e, 1, false, false) PO2Q_RK1(c, d, e, 2, true, false)
+    // the pipelined split (PIPE) for C = 64's MFMA-wave plans: default for the direct-store plans
+    // (0.159 vs 0.182 ms at bs 256 @56), not for the TT plans (no change there:
+    // profiles/r04_rowsk_pipe_ab.jsonl).  PO2Q_ROWSK_PIPE=0: never, 1: also with TT.
+    const int pipe = [] {
+        const char* e = getenv("PO2Q_ROWSK_PIPE");
+        return e ? atoi(e) : -1;
+    }();
+#define PO2Q_RKP(d, e, v, tt)                                                                                \
+    if ((pipe == 1 || (pipe < 0 && v == 1)) && p.C == 64 && p.pd == d && epi == e && p.vrx == v && !p.nts) { \
+        hipLaunchKernelGGL((conv_rowsk<64, d, tt, false, e, 0, 0, false, false, true>), dim3((unsigned)p.blocks), \
+                           dim3(kThreads), p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a); \
+        return hipGetLastError();                                                                            \
+    }
+    PO2Q_RKP(2, false, 2, true) PO2Q_RKP(3, false, 2, true) PO2Q_RKP(2, true, 2, true) PO2Q_RKP(3, true, 2, true)
+    PO2Q_RKP(2, false, 1, false) PO2Q_RKP(3, false, 1, false) PO2Q_RKP(2, true, 1, false) PO2Q_RKP(3, true, 1, false)
+#undef PO2Q_RKP
+    // ... and the direct-store plans with non-temporal stores / loads
+#define PO2Q_RKPN1(d, e, nt)                                                                                 \
+    if (pipe != 0 && p.C == 64 && p.pd == d && epi == e && p.vrx == 1 && p.nts == nt) {                      \
+        hipLaunchKernelGGL((conv_rowsk<64, d, false, false, e, 0, nt, false, false, true>), dim3((unsigned)p.blocks), \
+                           dim3(kThreads), p.lds_bytes, s, x, reinterpret_cast<const uint4*>(packed), scale, bias, y, a); \
+        return hipGetLastError();                                                                            \
+    }
+#define PO2Q_RKPN(d, e) PO2Q_RKPN1(d, e, 1) PO2Q_RKPN1(d, e, 2) PO2Q_RKPN1(d, e, 3)
+    PO2Q_RKPN(2, false) PO2Q_RKPN(3, false) PO2Q_RKPN(2, true) PO2Q_RKPN(3, true)
+#undef PO2Q_RKPN
+#undef PO2Q_RKPN1
 #ifdef PO2Q_ROWS_DIAG
     if (const char* dv = getenv("PO2Q_ROWSK_DEBUG")) {
         const int dbg = atoi(dv);
