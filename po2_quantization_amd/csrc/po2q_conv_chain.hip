@@ -122,6 +122,15 @@ struct ChainArgs {
 #endif
 
 
+// Packed fp32 (v_pk_fma / v_pk_add) in the epilogue and its exact split: on by default here (same
+// IEEE results either way; 1-2 % faster in the chain, 3 of 3 same-box rounds,
+// profiles/r04_chain_pk_ab.jsonl -- unlike the conv pair, po2q_conv_pair.hip); -DPO2Q_CHAIN_PK=0
+// builds the scalar form
+#ifndef PO2Q_CHAIN_PK
+#define PO2Q_CHAIN_PK 1
+#endif
+constexpr bool kChainPK = PO2Q_CHAIN_PK != 0;
+
 // C: channels; MG: most 16-pixel groups one wave owns (register arrays).  The activation lives
 // in LDS as split planes for the whole chain: per layer every wave first computes ALL its
 // groups' accumulators (transposed MFMA form, A = weights, B = pixels: each lane ends with 4
@@ -396,6 +405,16 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             float v[4];
 #pragma unroll
             for (int i = 0; i < 4; i += 2) {  // channel pairs as packed v_pk_fma / v_pk_add (the same IEEE ops)
+                if constexpr (!kChainPK) {
+#pragma unroll
+                    for (int e = i; e < i + 2; ++e) {
+                        float u = (acc[gi][e] * scale + cbk[e]) * ceps[e] + cepb[e];
+                        if (res_add) u += rres[gi][e];
+                        v[e] = epi_act(u, act);
+                        if (keep) rres[gi][e] = v[e];
+                    }
+                    continue;
+                }
                 const po2q_float2 sc = {scale, scale};
                 po2q_float2 u = (po2q_float2{acc[gi][i], acc[gi][i + 1]} * sc + po2q_float2{cbk[i], cbk[i + 1]}) *
                                     po2q_float2{ceps[i], ceps[i + 1]} +
@@ -417,7 +436,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 uint2 hi, mid, lo;
                 const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                                         __float_as_uint(v[3])};
-                split4p(vb, hi, mid, lo);
+                split4p<kChainPK>(vb, hi, mid, lo);
                 *reinterpret_cast<uint2*>(lds + wr + ad) = hi;
                 *reinterpret_cast<uint2*>(lds + wr + a.PL + ad) = mid;
                 *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
