@@ -174,6 +174,13 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                                                           const float* __restrict__ bias, float* __restrict__ y,
                                                           RowsKArgs a) {
     static_assert(!PIPE || (!LW && !RES && !FP && DBG == 0), "pipelined split: plain MFMA-wave plans");
+    // FPF (-DPO2Q_ROWSK_FPF=1, TT plans only: 2 blocks per CU leave the VGPRs for the second
+    // fragment set; the 3-block direct-store plans would spill): A fragments one k-step ahead.
+    // Off: no measurable change at stage 3 (profiles/r04_rowsk_pipe_ab.jsonl, call r04_24)
+#ifndef PO2Q_ROWSK_FPF
+#define PO2Q_ROWSK_FPF 0
+#endif
+    constexpr bool FPF = PO2Q_ROWSK_FPF != 0 && TT;
     constexpr int K = C;
     constexpr int NCH = C / 32;        // 32-channel chunks (k-steps per tap: one per chunk)
     constexpr int KSC = 3 * NCH;       // k-steps per tap row
@@ -432,15 +439,25 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         // (26 branches and ~110 s_waitcnt per step in the loop's ISA).
         auto mma = [&](auto G_, auto&& after0) __attribute__((always_inline)) {
             constexpr bool G = decltype(G_)::value;
-#pragma unroll
-            for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
-                bf16x8 af[3][NGW];
+            // A fragments one k-step ahead (FPF): k-step ks + 1's reads are issued before k-step ks's
+            // MFMAs, so their LDS latency runs under 3 x 3 x NGW MFMAs instead of stalling the first
+            bf16x8 af[2][3][NGW];
+            auto ldf = [&](bf16x8 (&f)[3][NGW], int ks) __attribute__((always_inline)) {
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                     for (int grp = 0; grp < NGW; ++grp)
-                        af[pl][grp] = __builtin_bit_cast(
-                            bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
+                        f[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + pl * PL + aoff[grp][ks]));
+            };
+            if constexpr (FPF && !(DBG & 2)) ldf(af[0], 0);
+#pragma unroll
+            for (int ks = 0; ks < KSC && !(DBG & 2); ++ks) {
+                bf16x8 (&cf)[3][NGW] = af[FPF ? (ks & 1) : 0];
+                if constexpr (FPF) {
+                    if (ks + 1 < KSC) ldf(af[(ks + 1) & 1], ks + 1);
+                } else {
+                    ldf(cf, ks);
+                }
 #pragma unroll
                 for (int rr = 0; rr < 3; ++rr) {
                     if (G && (j - rr < 0 || j - rr >= rbe)) continue;
@@ -448,7 +465,7 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
                     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                         for (int grp = 0; grp < NGW; ++grp)
-                            acc[SL[rr]][grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], bw[rr][ks],
+                            acc[SL[rr]][grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf[pl][grp], bw[rr][ks],
                                                                                       acc[SL[rr]][grp], 0, 0, 0);
                 }
                 if (ks == 0) after0();
@@ -722,6 +739,11 @@ hipError_t launch_conv_rowsk(const ConvPlan& p, const float* x, const uint16_t* 
     }
 #define PO2Q_RKDS(v) PO2Q_RKD(32, 3, true, false, v) PO2Q_RKD(32, 3, true, true, v)
         PO2Q_RKDS(6) PO2Q_RKDS(16) PO2Q_RKDS(2) PO2Q_RKDS(1) PO2Q_RKDS(7)
+#undef PO2Q_RKDS
+        // stage 3's TT plan (C = 64, 2 rows in flight)
+#define PO2Q_RKDS(v) PO2Q_RKD(64, 2, true, false, v)
+        PO2Q_RKDS(2) PO2Q_RKDS(4) PO2Q_RKDS(6) PO2Q_RKDS(16) PO2Q_RKDS(64) PO2Q_RKDS(128) PO2Q_RKDS(256)
+        PO2Q_RKDS(144) PO2Q_RKDS(400) PO2Q_RKDS(404) PO2Q_RKDS(148) PO2Q_RKDS(20) PO2Q_RKDS(132)
 #undef PO2Q_RKDS
 #undef PO2Q_RKD
     }
