@@ -146,6 +146,9 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 #ifndef PO2Q_PAIR_PK
 #define PO2Q_PAIR_PK 0
 #endif
+#ifndef PO2Q_PAIR_W2R
+#define PO2Q_PAIR_W2R 0
+#endif
 constexpr bool kPairPK = PO2Q_PAIR_PK != 0;
 
 template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0, int MW = 0>
@@ -296,6 +299,11 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     float scale1 = 1.0f, scale2 = 1.0f;
     bool fin1 = true, fin2 = true;
     bf16x8 bw1[NF], bw2[WL2 ? 1 : NF];
+    // C = 32, -DPO2Q_PAIR_W2R=1: conv 2's tap-row-0 B fragments also in VGPRs (the rest stay in
+    // LDS), a third fewer LDS weight reads per step.  Off: 0.353 vs 0.343 ms for the stage-2 pair and
+    // 2 % fewer images/s in the bench with it (226 VGPRs; profiles/r04_pair32_w2r_ab.jsonl)
+    constexpr int W2R = WL2 ? PO2Q_PAIR_W2R : 0;
+    bf16x8 bw2r[W2R ? KS * NT : 1];
     float bk1[E ? NT * 4 : 1], e1s[E ? NT * 4 : 1], e1b[E ? NT * 4 : 1];  // conv 1: ch 16 nt + 4 (lane >> 4) + e
     float bk2[NT], e2s[NT], e2b[NT];                                       // conv 2: ch 16 nt + (lane & 15)
     floatx4 acc1[3][NG][NT], acc2[3][NG][NT];
@@ -344,6 +352,8 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                     bf16x8 b;
                     if constexpr (TR)
                         b = bw[f];
+                    else if (WL2 && W2R && rr == 0)
+                        b = bw2r[W2R ? f : 0];
                     else if constexpr (WL2)
                         b = __builtin_bit_cast(bf16x8, wl2[f * 64 + lane]);
                     else
@@ -622,6 +632,11 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         scale2 = wq_prologue(a.q2, thr, red, nw + MW, fin2);
         if constexpr (WL2) {
             for (int e = tid; e < NF * 64; e += blockDim.x) wl2[e] = wq_frag_rows(a.q2, CC, CC, CC, NT, KS, e, scale2, fin2, thr);
+            if constexpr (W2R != 0) {
+#pragma unroll
+                for (int f = 0; f < KS * NT; ++f)
+                    bw2r[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
+            }
         } else {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
@@ -658,6 +673,10 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         if constexpr (!WL2) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw2[WL2 ? 0 : f]));
+        }
+        if constexpr (W2R != 0) {
+#pragma unroll
+            for (int f = 0; f < KS * NT; ++f) asm volatile("" : "+v"(bw2r[W2R ? f : 0]));
         }
         if constexpr (E == 2) {  // BasicBlock form: the conv scale and bias folded into the affine
 #pragma unroll
