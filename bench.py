@@ -11,8 +11,14 @@ Inputs and weights are synthetic (seeded)
 and resident in HBM before the timed region.  Each conv shape is autotuned
 on its first (untimed, warmup) call, as the reference's cudnn.benchmark does.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W]          (N > 1: starts N ranks itself, see below)
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process starts the N ranks itself:
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py ...` as a
+child process, before anything touches the GPU (importing po2_quantization_amd._lib loads no
+library), relays rank 0's JSON line and exits with the launcher's status.  Under a launcher the
+process group must hold exactly N ranks.
   python bench.py --image 32 --graph                     (config 2: CIFAR 32x32, hipGraph replay)
   torchrun ... bench.py --gpus 8 --global-batch 1024     (config 4: 128 images per GPU)
 
@@ -589,6 +595,46 @@ def model_cpu_baseline(m, image, seconds, label):
                       "conv / BN / act, %d threads), %.1f s" % (reps, nb, label, image, image, threads, dt)}
 
 
+def launch_ranks(n, argv):
+    """Start the N ranks of `bench.py argv` as one torch.distributed.run child process (one process
+    per GPU, rendezvous on 127.0.0.1) and return its exit status.  Called before any GPU call: this
+    parent only waits (no exec from a process that initialised the GPU)."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box's driver supports dmabuf IPC only
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def selftest(args, world, rank, backend):
+    """--selftest: the N-rank plumbing of the step without any kernel (CPU tensors, gloo): every rank's
+    batch shard of stand-in logits (a deterministic function of the rank), the all_gather of the
+    outputs and the barrier-bracketed max-over-ranks timing of timed_steps.  Rank 0 checks the gathered
+    logits against every shard and prints one JSON line (tests/test_distributed.py runs it through the
+    --gpus 2 entry)."""
+    B, classes = 4, 10
+    dev = torch.device("cpu")
+
+    def shard(r):
+        return torch.arange(B * classes, dtype=torch.float32).view(B, classes) * (r + 1) + 1000.0 * r
+
+    logits = shard(rank)
+    gathered = torch.empty(world * B, classes)
+    dt = timed_steps(lambda record=False: gather_logits(logits, gathered, world), args.steps, args.warmup, world,
+                     lambda: None, dev)
+    out = gather_logits(logits, gathered, world) if world > 1 else logits
+    expect = torch.cat([shard(r) for r in range(world)])
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "world_size": world, "dist_backend": backend,
+                          "gathered_ok": bool(torch.equal(out, expect)), "gathered_rows": int(out.shape[0]),
+                          "steps": args.steps, "seconds": dt}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -621,7 +667,18 @@ def main():
     ap.add_argument("--no-models", dest="models", action="store_false",
                     help="skip the model-config lines (config 3: MobileNetV2 @32 po2+ 4-bit; config 5: MobileViT-XS "
                          "@256 po2+ 2-bit), reported under config3_mobilenet32 / config5_mobilevit256")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI on ROCm)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="N-rank plumbing only (gloo, CPU stand-in logits, no kernels): launcher, gather, timing")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the N ranks (nothing has touched the GPU in this process)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.selftest:
+        args.backend = "gloo"
     # the reference runs with torch.backends.cudnn.benchmark = True (train.py:33, test.py:31);
     # the po2q counterpart times every candidate plan on a shape's first call (an untimed warmup step)
     _lib.benchmark = not args.no_autotune
@@ -632,10 +689,21 @@ def main():
     backend = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         # what the process group itself reports (the env only says what torchrun asked for)
         world, rank, backend = dist.get_world_size(), dist.get_rank(), str(dist.get_backend())
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the process group holds %d ranks" % (args.gpus, world))
+    if args.selftest:
+        selftest(args, world, rank, backend)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -803,10 +871,12 @@ def main():
         "layer_roofline": layer_roof,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baselines run on rank 0 after each timed region (the other ranks wait at the next
+    # barrier), at every N
+    cpu_leg = rank == 0 and not args.no_cpu_baseline
+    if cpu_leg:
         wcpu = [w.cpu() for w in chain.weights]
         out["cpu_baseline"] = cpu_baseline(chain.layers, wcpu, Hs, args.quantizer, args.bits, args.cpu_seconds)
-    cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline
     if args.cifar and Hs != 32:
         del chain, x, xl
         torch.cuda.empty_cache()

@@ -25,6 +25,7 @@ built and the BatchNorms are in eval mode; otherwise they run the reference's mo
 sequence unchanged.
 """
 import contextlib
+import threading
 
 import torch
 import torch.nn as nn
@@ -166,12 +167,21 @@ def can_fuse(*mods):
 # records which layers do that and at which shapes; later forwards at that shape pack them
 # up front.  False: every layer packs its own weight (A/B runs).
 BATCHED_PACKS = True
-_packs = None  # the active forward's _ForwardPacks (None outside batched_packs)
+# The active forward's _ForwardPacks, per thread: concurrent eval forwards (threads, DataParallel
+# replicas) each see only their own session.
+_tls = threading.local()
+
+
+def _session(module):
+    """The calling thread's active _ForwardPacks when `module` belongs to the model that opened it."""
+    sess = getattr(_tls, "packs", None)
+    return sess if sess is not None and id(module) in sess.owned else None
 
 
 class _ForwardPacks:
-    def __init__(self, layers):
+    def __init__(self, model, layers):
         self.recording = [] if layers is None else None
+        self.owned = {id(m) for m in model.modules()}
         self.ws = {}
         self.fixed = {}  # id(conv) -> plan index while recording an inverted-residual block's layers
         if layers is None:
@@ -179,29 +189,43 @@ class _ForwardPacks:
         groups = {}
         for m, g, conf, plan in layers:
             groups.setdefault(conf, []).append((m, g, plan))
-        for (bits, mode, prec), items in groups.items():
+        for conf, items in groups.items():
+            bits, mode, prec = conf
             ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g, _ in items], bits, mode, 1, prec,
                                  plans=[pl for _, _, pl in items])
             for (m, g, pl), w in zip(items, ws):
-                self.ws[id(m)] = (g, m.weight, w, pl)
+                self.ws[id(m)] = (g, m.weight, w, pl, conf)
+
+    def lookup(self, conv, g, weight):
+        """The pack of `conv` when it was made for this geometry, this weight tensor and the layer's
+        current (bits, mode, precision); None otherwise (the caller packs the layer itself)."""
+        hit = self.ws.get(id(conv))
+        if hit is None or hit[0] != g or hit[1] is not weight or hit[2].numel() == 0:
+            return None
+        if hit[4] != (conv.bits, NATIVE_MODES.get(conv.quantize_fn), conv.precision):
+            return None
+        return hit
 
 
 @contextlib.contextmanager
 def batched_packs(model, x):
     """Run a model's eval forward with its single-conv layers' weight packs batched (BATCHED_PACKS)."""
-    global _packs
-    if (not BATCHED_PACKS or _packs is not None or torch.is_grad_enabled() or model.training
+    if (not BATCHED_PACKS or getattr(_tls, "packs", None) is not None or torch.is_grad_enabled() or model.training
             or not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32)):
         yield
         return
-    key = (tuple(x.shape), x.device, INFERENCE_FUSION, IR_FUSION)
+    # the record holds which layers read a packed weight and with which plan; it depends on the
+    # layers' quantizer settings and precision as much as on the input shape
+    confs = tuple((m.bits, NATIVE_MODES.get(m.quantize_fn), m.precision) for m in model.modules()
+                  if isinstance(m, QuantizedConv2d))
+    key = (tuple(x.shape), x.device, INFERENCE_FUSION, IR_FUSION, confs)
     rec = model.__dict__.setdefault("_po2q_packs", {})
-    sess = _ForwardPacks(rec.get(key))
-    _packs = sess
+    sess = _ForwardPacks(model, rec.get(key))
+    _tls.packs = sess
     try:
         yield
     finally:
-        _packs = None
+        _tls.packs = None
     if sess.recording is not None:
         rec[key] = sess.recording
 
@@ -272,14 +296,14 @@ class QuantizedConv2d(nn.Conv2d):
             weight = self.quantize_fn.apply(self.weight, self.bits)
             mode = "none"
         ps, pb = fold_bn(bn) if bn is not None else (None, None)
-        sess = _packs
+        sess = _session(self)
         if sess is not None and mode != "none" and input.dim() == 4:
             g = (tuple(input.shape), tuple(self.stride), tuple(self._padding(input)), tuple(self.dilation), self.groups)
             if sess.recording is not None:
                 sess.recording.append((self, g, (self.bits, mode, self.precision), sess.fixed.get(id(self))))
             else:
-                hit = sess.ws.get(id(self))
-                if hit is not None and hit[0] == g and hit[1] is weight and hit[2].numel() > 0:
+                hit = sess.lookup(self, g, weight)
+                if hit is not None:
                     return _lib.qconv2d_packed(input, weight, hit[2], self.bias, g[1], g[2], g[3], g[4], self.bits,
                                                mode, 1, self.precision, post_scale=ps, post_shift=pb,
                                                residual=residual, act=act or "none", plan=hit[3])
@@ -295,6 +319,18 @@ class QuantizedConv2d(nn.Conv2d):
         else:
             return 0, self.weight.numel()
 
+
+
+def plain_conv(conv, x):
+    """An unquantized nn.Conv2d (the reference's stems: resnet.py:99-102) on a HIP fp32 input through
+    the native fp32 kernels with the native backward (_QConv2dFn, mode "none": exact fp32 products,
+    the weight gradient from the fixed-order wgrad kernels, so a training step is deterministic run to
+    run); any other input runs the module itself."""
+    if (not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4) or conv.padding_mode != "zeros"
+            or isinstance(conv.padding, str)):
+        return conv(x)
+    return _QConv2dFn.apply(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, 4,
+                            "none", "auto")
 
 
 def plain_conv_fused(conv, x, bn=None, act=None, residual=None):
@@ -404,7 +440,7 @@ def run_inverted_residual(seq, x, residual=None):
     """run_fused_sequence(seq, x, residual) for an inverted-residual conv block: ONE qconv2d_ir launch
     when a batched_packs forward holds the three layers' packs, else the per-layer fused calls
     (which record the layers for the next forward's packs)."""
-    sess = _packs
+    sess = _session(seq)
     spec = _ir_spec(seq) if IR_FUSION and sess is not None else None
     if spec is not None and x.dim() == 4:  # only blocks the kernel takes: the others keep their tuned plans
         d = spec[1][0]
@@ -422,8 +458,10 @@ def run_inverted_residual(seq, x, residual=None):
         hits = []
         for g in spec:
             hit = sess.ws.get(id(g[0])) if g is not None else None
-            if g is not None and (hit is None or hit[1] is not g[0].weight or hit[2].numel() == 0 or hit[3] != 0):
-                break
+            if g is not None:
+                hit = sess.lookup(g[0], hit[0], g[0].weight) if hit is not None else None
+                if hit is None or hit[3] != 0:
+                    break
             hits.append(hit)
         else:
             e, d, p = spec

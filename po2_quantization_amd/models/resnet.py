@@ -19,7 +19,8 @@ import torch.nn as nn
 
 from .. import _lib
 from ..utils.quantizers import NATIVE_MODES
-from .quantized_conv import QuantizedConv2d, batched_packs, can_fuse, fold_bn, plain_conv_fused, run_fused_sequence
+from .quantized_conv import (QuantizedConv2d, batched_packs, can_fuse, fold_bn, plain_conv, plain_conv_fused,
+                             run_fused_sequence)
 
 
 class BasicBlock(nn.Module):
@@ -148,7 +149,7 @@ class ResNet(nn.Module):
                 # the unquantized stem conv + bn1 + relu (resnet.py:99-102, 191) as one native fp32 call
                 x = plain_conv_fused(self.conv1, x, bn=self.bn1, act="relu")
             else:
-                x = self.relu(self.bn1(self.conv1(x)))
+                x = self.relu(self.bn1(plain_conv(self.conv1, x)))  # native forward + backward
             for layer in (self.layer1, self.layer2, self.layer3):
                 x = self._stage(layer, x)
         return self.fc(torch.flatten(self.avgpool(x), 1))

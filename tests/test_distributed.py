@@ -100,5 +100,39 @@ def test_sharded_qconv_chain_equals_full_batch(tmp_path, monkeypatch):
         assert torch.allclose(res[r]["gathered"], full, rtol=1e-5, atol=1e-6)
 
 
+def test_bench_entry_starts_n_ranks():
+    """`python bench.py --gpus 2` (the driver's command shape) starts the two ranks itself through
+    torch.distributed.run and relays rank 0's line: the process group holds 2 ranks, and rank 0 holds
+    both shards' outputs after the all_gather.  --selftest runs the plumbing with CPU stand-in logits
+    over gloo (no kernels here); the GPU box runs the same entry over RCCL."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--selftest", "--steps", "3",
+                        "--warmup", "1"], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["world_size"] == 2 and out["n_gpus"] == 2 and out["dist_backend"] == "gloo", out
+    assert out["gathered_ok"] and out["gathered_rows"] == 8, out
+
+
+def test_bench_entry_rejects_world_mismatch():
+    """Under an external launcher the process group must hold exactly --gpus ranks."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--selftest"], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "process group holds 1 ranks" in r.stderr, r.stderr[-2000:]
+
+
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])

@@ -34,14 +34,33 @@ def build(spec, q, bits):
                                          ("mobilenet", "po2+", 4), ("mobilenet", "po2", 2),
                                          ("mobilevit", "po2+", 2), ("mobilevit", "po2", 4),
                                          ("mobilevit@64", "po2+", 2)])
-def test_qat_mode_logits(spec, q, bits):
+def test_qat_mode_logits(spec, q, bits, monkeypatch):
+    """Three eval forwards at one shape: the first records which layers read a packed weight
+    (models/quantized_conv.py batched_packs), the later ones run the path the bench and users run
+    from then on -- the batched weight packs and, for MobileNetV2, the fused inverted-residual block
+    kernel at its 4x4 blocks (asserted to run).  Every forward's logits against the reference's."""
+    from po2_quantization_amd import _lib
+
+    calls = {"ir": 0, "packed": 0}
+    ir, packed = _lib.qconv2d_ir, _lib.qconv2d_packed
+    monkeypatch.setattr(_lib, "qconv2d_ir", lambda *a, **k: calls.__setitem__("ir", calls["ir"] + 1) or ir(*a, **k))
+    monkeypatch.setattr(_lib, "qconv2d_packed",
+                        lambda *a, **k: calls.__setitem__("packed", calls["packed"] + 1) or packed(*a, **k))
     d = load_npz("models.npz")
     m = build(spec, q, bits)
-    x = d["x/img64"] if spec.endswith("@64") else d["x/cifar8"]
-    with torch.no_grad():
-        y = m(torch.from_numpy(x).to(DEV)).cpu().numpy()
+    x = torch.from_numpy(d["x/img64"] if spec.endswith("@64") else d["x/cifar8"]).to(DEV)
     ref = d["logits/%s/%s/%d" % (spec, q or "none", bits)]
-    assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
+    with torch.no_grad():
+        y1 = m(x).cpu().numpy()
+        assert calls == {"ir": 0, "packed": 0}  # the recording forward: per-layer calls
+        y2 = m(x).cpu().numpy()
+        y3 = m(x).cpu().numpy()
+    for y in (y1, y2, y3):
+        assert normwise_err(y, ref) <= LOGIT_TOL, normwise_err(y, ref)
+    if q is not None:
+        assert calls["packed"] > 0, calls  # the second forward ran from the batched packs
+    if spec == "mobilenet":
+        assert calls["ir"] >= 2, calls  # the 4x4 blocks as one qconv2d_ir launch each, in both later forwards
 
 
 @pytest.mark.parametrize("spec,q,bits,n", [("resnet56", "po2", 4, 9), ("resnet20", "po2+", 3, 3)])
@@ -159,7 +178,7 @@ def test_wide_resnet_logits_through_fused_block_kernels(tag, pair_c32, monkeypat
     assert normwise_err(y, d["logits/" + tag]) <= LOGIT_TOL, normwise_err(y, d["logits/" + tag])
 
 
-def test_mobilevit_256_logits_config5():
+def test_mobilevit_256_logits_config5(monkeypatch):
     """BASELINE config 5 at its own size: MobileViT-XS @256x256, 1000 classes, po2+ 2-bit QAT-mode
     weights (the reference quantizes no activations), eval forward with every conv + BN + act native,
     against the reference's logits (tests/golden/models_vit256.npz; reference models/mobile_vit.py:
@@ -171,6 +190,14 @@ def test_mobilevit_256_logits_config5():
     m = get_model("mobilevit", 1000, quantizer_dict["po2+"], 2, (256, 256))
     seeded_fill_(m, seed=7)
     m = m.to(DEV).eval()
+    from po2_quantization_amd import _lib
+
+    n = [0]
+    packed = _lib.qconv2d_packed
+    monkeypatch.setattr(_lib, "qconv2d_packed", lambda *a, **k: n.__setitem__(0, n[0] + 1) or packed(*a, **k))
     with torch.no_grad():
-        y = m(x.to(DEV)).cpu().numpy()
-    assert normwise_err(y, d["logits/" + tag]) <= LOGIT_TOL, normwise_err(y, d["logits/" + tag])
+        y1 = m(x.to(DEV)).cpu().numpy()  # records
+        y2 = m(x.to(DEV)).cpu().numpy()  # batched packs (the path config 5's bench replays)
+    assert n[0] > 0
+    for y in (y1, y2):
+        assert normwise_err(y, d["logits/" + tag]) <= LOGIT_TOL, normwise_err(y, d["logits/" + tag])

@@ -211,9 +211,10 @@ def test_pair_role_split_kernel(W, monkeypatch):
                                    (1, 112, 112, 32), (2, 7, 100, 32)])
 def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     """The memory-wave kernel (PO2Q_PAIR_MW = ring slots: an eighth wave issues every x DMA, the
-    compute waves issue none) moves the loads, not the arithmetic: bit for bit the default kernel's
-    output, plain and with the general (BN + activation) epilogue; and within the bar of torch's
-    fp32 chain on Q(w)."""
+    compute waves issue none) moves the loads, not the arithmetic: bit for bit the one-role kernel's
+    output (PO2Q_PAIR_MW=0: every compute wave DMAs its own share of the x rows; at C = 16 the
+    default is the memory wave itself), plain and with the general (BN + activation) epilogue; and
+    within the bar of torch's fp32 chain on Q(w)."""
     N, H, W, C = shape
     if C == 32 and pd > 5:
         pytest.skip("C = 32: at most 5 ring slots fit the LDS")
@@ -223,7 +224,7 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
         forms += [dict(act1="relu", act2="relu", residual=x, **e), dict(act1="relu6", act2="silu", residual=x, **e)]
     outs = []
     for kw in forms:
-        monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
+        monkeypatch.setenv("PO2Q_PAIR_MW", "0")
         ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
         monkeypatch.setenv("PO2Q_PAIR_MW", str(pd))
         y = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
@@ -231,3 +232,6 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
         outs.append(y)
     t = torch_chain(x, w1, w2, e, "relu", "relu6", None)  # forms[1]
     assert nerr(outs[1], t) <= CONV_TOL
+    if C == 16 and W > 192 and pd == 5:  # 7-wave widths: with PO2Q_PAIR_MW unset the default is MW at PD 5
+        monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
+        assert torch.equal(_lib.qconv2d_pair(x, w1, w2, 4, "po2"), outs[0])
