@@ -304,6 +304,14 @@ static int run_plan(const ConvPlan& p, const float* x, const float* w, const flo
     return hip_status(launch_epilogue(y, p.N, p.K, (int64_t)p.P * p.Q, e, false, s), "epilogue launch");
 }
 
+// Whether run_plan needs its own elementwise pass over y for an eval epilogue (BN affine + activation,
+// no residual): the plans whose conv kernel cannot apply it in its stores.
+static bool plan_needs_epilogue_pass(const ConvPlan& p) {
+    if (p.kind == KIND_BF16X3_PW || p.kind == KIND_BF16X3_IMG || p.kind == KIND_BF16X3_ROWS) return false;
+    if (p.kind == KIND_DIRECT_F32 || p.kind == KIND_PW_F32 || p.kind == KIND_DEPTHWISE) return false;
+    return true;  // bf16x3 tile / DMA kernels, the fp32 MFMA kernel
+}
+
 static const char* kKindNames[] = {"mfma_f32", "depthwise", "bf16x3", "bf16x3_dma", "bf16x3_rows", "bf16x3_pw",
                                    "direct_f32", "pw_f32", "bf16x3_img"};
 
@@ -399,6 +407,28 @@ int po2q_qconv2d_autotune(const float* x, const float* w, const float* bias, flo
             }
         }
     }
+    // The model forwards call almost every conv with the eval BatchNorm (+ activation) after it
+    // (QuantizedConv2d.fused): a plan that cannot apply it in its stores pays one more pass over y.
+    // Charge that pass (timed once here: read + write of y) to those plans, so e.g. an unquantized
+    // stem takes the direct kernel with its fused epilogue over an fp32 MFMA plan that is faster
+    // alone but needs the pack, the conv and the pass (31 vs ~10 us, MobileNetV2 @32).
+    float epi_ms = 0.f;
+    if (!st) {
+        bool any = false;
+        for (const ConvPlan& c : cands) any = any || plan_needs_epilogue_pass(c);
+        const ConvEpi ep{nullptr, nullptr, nullptr, PO2Q_ACT_RELU};
+        for (int r = 0; any && r < 3 && !st; ++r) {
+            st = hip_status(hipEventRecord(e0, s), "event record");
+            if (!st) st = hip_status(launch_epilogue(y, N, K, (int64_t)cands[0].P * cands[0].Q, ep, false, s), "epilogue");
+            if (!st) st = hip_status(hipEventRecord(e1, s), "event record");
+            if (!st) st = hip_status(hipEventSynchronize(e1), "autotune run");
+            float ms = 0.f;
+            if (!st) st = hip_status(hipEventElapsedTime(&ms, e0, e1), "event time");
+            if (!st && r > 0) epi_ms = r == 1 ? ms : std::min(epi_ms, ms);
+        }
+    }
+    for (int i = 0; i < (int)cands.size(); ++i)
+        if (plan_needs_epilogue_pass(cands[i])) tmin[i] += epi_ms;
     for (int i = 0; i < (int)cands.size(); ++i)
         if (best < 0 || tmin[i] < tmin[best]) best = i;
     // within 1 % (timing noise), prefer a plan with fused weight staging: one launch per
@@ -646,6 +676,7 @@ int po2q_qconv2d_plan_pack_batch(int n, const po2q_conv_plan* const* plans, cons
         char* ws = reinterpret_cast<char*>(workspace[i]);
         reqs.push_back(PackReq{&p, w[i], ws + L.packed_off, reinterpret_cast<float*>(ws + L.scale_off), h->bits, h->fsr,
                                h->mode});
+        reqs.back().partial = reinterpret_cast<unsigned*>(ws);  // the layout's absmax partials (part_bytes)
     }
     if (reqs.empty()) return PO2Q_OK;
     return hip_status(launch_pack_batch((int)reqs.size(), reqs.data(), s), "batched weight pack launch");

@@ -45,7 +45,6 @@ namespace po2q {
 
 namespace {
 constexpr int kChainThreads = 512;  // 8 waves: two per SIMD
-constexpr int kChainItems = 5;      // split items (pixel x channel octet) per thread and load batch
 constexpr int kChainMax = PO2Q_CHAIN_MAX_LAYERS;
 constexpr size_t kChainLdsMax = 160 * 1024;
 
@@ -168,32 +167,62 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     const float* xn = x + (int64_t)n * img;
     float* yn = y + (int64_t)n * img;
 
-    // ---- x -> split planes, the zero halo with it (written once: later layers write interiors)
-    const int nitems = (H + 2) * PW * NO;
-    for (int base = 0; base < nitems; base += kChainThreads * kChainItems) {
-        uint32_t v[kChainItems][8];
-        int dst[kChainItems];
+    // ---- x -> split planes (written once: later layers write interiors).  A lane takes 4 consecutive
+    // pixels x 8 channels: 8 float4 loads (where one pixel per lane took 8 scattered dword loads per
+    // 8 values), then the split of each pixel's 8 channels into its octet of the 3 planes.  The
+    // zero halo (padded rows 0 / H + 1, columns 0 / W + 1) is written by a pass of its own.
+    {
+        const int W4 = W >> 2;
+        const int nq = H * W4 * NO;  // interior quads x channel octets (W % 4 == 0, host-checked)
+        const bool xaligned = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;  // block-uniform
+        for (int it = tid; it < nq; it += kChainThreads) {
+            const int q4 = it % W4, t = it / W4;
+            const int h = t % H, oc = t / H;
+            const float* src = xn + (int64_t)(8 * oc) * HW + h * W + 4 * q4;
+            float4 v4[8];
+            if (xaligned) {
 #pragma unroll
-        for (int i = 0; i < kChainItems; ++i) {
-            const int it = base + i * kChainThreads + tid;
-            const bool ok = it < nitems;
-            const int pc = it % PW, t = it / PW;
-            const int rr = t % (H + 2), oc = t / (H + 2);
-            const int h = rr - 1, xc = pc - 1;
-            const bool inb = ok && h >= 0 && h < H && xc >= 0 && xc < W;
-            const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
+                for (int e = 0; e < 8; ++e) v4[e] = *reinterpret_cast<const float4*>(src + (int64_t)e * HW);
+            } else {  // an input view that is not 16-byte aligned: dword loads
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
-            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc) : -1;
+                for (int e = 0; e < 8; ++e) {
+                    const float* r = src + (int64_t)e * HW;
+                    v4[e] = make_float4(r[0], r[1], r[2], r[3]);
+                }
+            }
+#pragma unroll
+            for (int px = 0; px < 4; ++px) {
+                uint32_t v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    v[e] = __float_as_uint(px == 0 ? v4[e].x : px == 1 ? v4[e].y : px == 2 ? v4[e].z : v4[e].w);
+                const int pc = 4 * q4 + px + 1;
+                const int dst = ch_addr<C, W8, S16>((h + 1) * PW + pc, pc, oc);
+                uint4 hi, mid, lo;
+                split3(v, hi, mid, lo);
+                *reinterpret_cast<uint4*>(lds + dst) = hi;
+                *reinterpret_cast<uint4*>(lds + a.PL + dst) = mid;
+                *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst) = lo;
+            }
         }
-#pragma unroll
-        for (int i = 0; i < kChainItems; ++i) {
-            if (dst[i] < 0) continue;
-            uint4 hi, mid, lo;
-            split3(v[i], hi, mid, lo);
-            *reinterpret_cast<uint4*>(lds + dst[i]) = hi;
-            *reinterpret_cast<uint4*>(lds + a.PL + dst[i]) = mid;
-            *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst[i]) = lo;
+        // the zero halo: rows 0 and H + 1 (every padded column), columns 0 and W + 1 (rows 1 .. H)
+        const int nb = (2 * PW + 2 * H) * NO;
+        for (int it = tid; it < nb; it += kChainThreads) {
+            const int oc = it % NO, b = it / NO;
+            int rr, pc;
+            if (b < 2 * PW) {
+                rr = b < PW ? 0 : H + 1;
+                pc = b < PW ? b : b - PW;
+            } else {
+                const int k = b - 2 * PW;
+                rr = 1 + (k >> 1);
+                pc = (k & 1) ? W + 1 : 0;
+            }
+            const int dst = ch_addr<C, W8, S16>(rr * PW + pc, pc, oc);
+            const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+            *reinterpret_cast<uint4*>(lds + dst) = z;
+            *reinterpret_cast<uint4*>(lds + a.PL + dst) = z;
+            *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst) = z;
         }
     }
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.PL + a.ZO) = make_uint4(0u, 0u, 0u, 0u);
@@ -396,52 +425,65 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         }
         CHS(2);
 
-        // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p
+        // ---- epilogue: lane = channels c0 .. c0 + 3 of pixel 16 grp + p.  The activation and the
+        // residual add are compile-time inside (one dispatch per layer): a runtime activation switch
+        // per value had put ~6 scalar branches beside every value (the epilogue took 1.3x the MFMA
+        // phase, profiles/r04_chain_stamps.txt)
+        auto epilogue = [&](auto ACT_, auto RA_) __attribute__((always_inline)) {
+            constexpr int ACT = decltype(ACT_)::value;
+            constexpr bool RA = decltype(RA_)::value;
 #pragma unroll
-        for (int gi = 0; gi < MG; ++gi) {
-            const int grp = gsub + gi * WPT;
-            const int f = 16 * grp + p;
-            if (!FULL && (grp >= ngroups || f >= HW)) continue;
-            float v[4];
+            for (int gi = 0; gi < MG; ++gi) {
+                const int grp = gsub + gi * WPT;
+                const int f = 16 * grp + p;
+                if (!FULL && (grp >= ngroups || f >= HW)) continue;
+                float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; i += 2) {  // channel pairs as packed v_pk_fma / v_pk_add (the same IEEE ops)
-                if constexpr (!kChainPK) {
+                for (int i = 0; i < 4; i += 2) {  // channel pairs as packed v_pk_fma / v_pk_add (the same IEEE ops)
+                    if constexpr (!kChainPK) {
 #pragma unroll
-                    for (int e = i; e < i + 2; ++e) {
-                        float u = (acc[gi][e] * scale + cbk[e]) * ceps[e] + cepb[e];
-                        if (res_add) u += rres[gi][e];
-                        v[e] = epi_act(u, act);
-                        if (keep) rres[gi][e] = v[e];
+                        for (int e = i; e < i + 2; ++e) {
+                            float u = (acc[gi][e] * scale + cbk[e]) * ceps[e] + cepb[e];
+                            if constexpr (RA) u += rres[gi][e];
+                            v[e] = epi_act_ct<ACT>(u);
+                        }
+                        continue;
                     }
-                    continue;
+                    const po2q_float2 sc = {scale, scale};
+                    po2q_float2 u = (po2q_float2{acc[gi][i], acc[gi][i + 1]} * sc + po2q_float2{cbk[i], cbk[i + 1]}) *
+                                        po2q_float2{ceps[i], ceps[i + 1]} +
+                                    po2q_float2{cepb[i], cepb[i + 1]};
+                    if constexpr (RA) u += po2q_float2{rres[gi][i], rres[gi][i + 1]};
+                    v[i] = epi_act_ct<ACT>(u.x);
+                    v[i + 1] = epi_act_ct<ACT>(u.y);
                 }
-                const po2q_float2 sc = {scale, scale};
-                po2q_float2 u = (po2q_float2{acc[gi][i], acc[gi][i + 1]} * sc + po2q_float2{cbk[i], cbk[i + 1]}) *
-                                    po2q_float2{ceps[i], ceps[i + 1]} +
-                                po2q_float2{cepb[i], cepb[i + 1]};
-                if (res_add) u += po2q_float2{rres[gi][i], rres[gi][i + 1]};
-                v[i] = epi_act(u.x, act);
-                v[i + 1] = epi_act(u.y, act);
-                if (keep) {
-                    rres[gi][i] = v[i];
-                    rres[gi][i + 1] = v[i + 1];
-                }
-            }
-            if (last) {
+                if (keep) {  // wave-uniform
 #pragma unroll
-                for (int i = 0; i < 4; ++i) yn[(int64_t)(c0 + i) * HW + f] = v[i];
-            } else {
-                const int oy = f / W, ox = f - oy * W;
-                const int ad = ch_addr<C, W8, S16>((oy + 1) * PW + ox + 1, ox + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
-                uint2 hi, mid, lo;
-                const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                        __float_as_uint(v[3])};
-                split4p<kChainPK>(vb, hi, mid, lo);
-                *reinterpret_cast<uint2*>(lds + wr + ad) = hi;
-                *reinterpret_cast<uint2*>(lds + wr + a.PL + ad) = mid;
-                *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
+                    for (int e = 0; e < 4; ++e) rres[gi][e] = v[e];
+                }
+                if (last) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) yn[(int64_t)(c0 + i) * HW + f] = v[i];
+                } else {
+                    // padded pixel (oy + 1, ox + 1) of output pixel f = (oy, ox): pp0 / px0 hold (oy, ox) of
+                    // tap (0, 0), so no division by W here
+                    const int ad = ch_addr<C, W8, S16>(pp0[gi] + PW + 1, px0[gi] + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
+                    uint2 hi, mid, lo;
+                    const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                            __float_as_uint(v[3])};
+                    split4p<kChainPK>(vb, hi, mid, lo);
+                    *reinterpret_cast<uint2*>(lds + wr + ad) = hi;
+                    *reinterpret_cast<uint2*>(lds + wr + a.PL + ad) = mid;
+                    *reinterpret_cast<uint2*>(lds + wr + 2 * a.PL + ad) = lo;
+                }
             }
-        }
+        };
+        with_act(act, [&](auto ACT_) __attribute__((always_inline)) {
+            if (res_add)
+                epilogue(ACT_, std::true_type{});
+            else
+                epilogue(ACT_, std::false_type{});
+        });
         CHS(3);
         // the next layer's input planes are complete (the block's own LDS writes: lgkmcnt)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

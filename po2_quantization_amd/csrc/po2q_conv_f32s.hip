@@ -36,8 +36,12 @@ struct F32sArgs {
     int act;
 };
 
+// ACT: -1 = no epilogue (bias only), else the eval affine / residual / activation ACT (compile-time:
+// a runtime activation switch per value had put ~400 scalar branches into the stem kernel)
+template <int ACT>
 __device__ __forceinline__ void f32s_store4(const F32sArgs& a, float* __restrict__ y, int n, int k, int p, int q,
-                                            float (&v)[4], const float* __restrict__ bias, bool epi) {
+                                            float (&v)[4], const float* __restrict__ bias) {
+    constexpr bool epi = ACT >= 0;
     const float bk = bias ? bias[k] : 0.0f;
     const float s = (epi && a.ps) ? a.ps[k] : 1.0f;
     const float t = (epi && a.pb) ? a.pb[k] : 0.0f;
@@ -45,16 +49,16 @@ __device__ __forceinline__ void f32s_store4(const F32sArgs& a, float* __restrict
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         v[e] += bk;
-        if (epi) v[e] = v[e] * s + t;
+        if constexpr (epi) v[e] = v[e] * s + t;
     }
     if ((a.Q & 3) == 0) {  // q is a multiple of 4: one aligned float4
         if (epi && a.res) {
             const float4 r = *reinterpret_cast<const float4*>(a.res + off);
             v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         }
-        if (epi) {
+        if constexpr (epi) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act);
+            for (int e = 0; e < 4; ++e) v[e] = epi_act_ct<epi ? ACT : 0>(v[e]);
         }
         *reinterpret_cast<float4*>(y + off) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
@@ -63,22 +67,25 @@ __device__ __forceinline__ void f32s_store4(const F32sArgs& a, float* __restrict
             if (q + e >= a.Q) break;
             float u = v[e];
             if (epi && a.res) u += a.res[off + e];
-            if (epi) u = epi_act(u, a.act);
+            if constexpr (epi) u = epi_act_ct<epi ? ACT : 0>(u);
             y[off + e] = u;
         }
     }
 }
 
 // Direct 3x3 conv, C <= 4 input channels, stride SH, pad (ph, pw): thread = (image n, output
-// row p, 4 output columns q0 .. q0 + 3) x the 16 output channels of blockIdx.y.
-template <int SH, int CMAX>
+// row p, 4 output columns q0 .. q0 + 3) x the KB output channels of blockIdx.y.  KB 16: the
+// large stems (ResNet @224: 3.2 M threads); KB 4: small images, where 16 channels per thread left
+// half the chip idle and each thread four dependent weight batches long (MobileNetV2 @32's stem:
+// 128 blocks, 31 us).
+template <int SH, int CMAX, int KB = 16>
 __global__ __launch_bounds__(256) void conv_direct_f32(const float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ y,
                                                        F32sArgs a, int epi) {
     constexpr int IC = (4 - 1) * SH + 3;  // input columns the 4 outputs touch
     const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t >= a.items) return;
-    const int k0 = (int)blockIdx.y * 16;
+    const int k0 = (int)blockIdx.y * KB;
     const int q4 = t % a.Q4;
     const int rest = t / a.Q4;
     const int p = rest % a.P, n = rest / a.P;
@@ -100,58 +107,73 @@ __global__ __launch_bounds__(256) void conv_direct_f32(const float* __restrict__
             }
         }
     }
-    const bool ep = epi != 0;
+    auto body = [&](auto ACT_) __attribute__((always_inline)) {
+        constexpr int ACT = decltype(ACT_)::value;
 #pragma unroll 1
-    for (int kk = 0; kk < 16; kk += 4) {
-        float acc[4][4];
+        for (int kk = 0; kk < KB; kk += 4) {
+            float acc[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[u][e] = 0.0f;
+                for (int e = 0; e < 4; ++e) acc[u][e] = 0.0f;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = k0 + kk + u;
-            const int kc = k < a.K ? k : 0;  // wave-uniform
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + kk + u;
+                const int kc = k < a.K ? k : 0;  // wave-uniform
 #pragma unroll
-            for (int c = 0; c < CMAX; ++c) {
-                if (c >= a.C) break;
+                for (int c = 0; c < CMAX; ++c) {
+                    if (c >= a.C) break;
 #pragma unroll
-                for (int r = 0; r < 3; ++r)
+                    for (int r = 0; r < 3; ++r)
 #pragma unroll
-                    for (int s = 0; s < 3; ++s) {
-                        const float wt = w[((kc * a.C + c) * 3 + r) * 3 + s];
+                        for (int s = 0; s < 3; ++s) {
+                            const float wt = w[((kc * a.C + c) * 3 + r) * 3 + s];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) acc[u][e] = fmaf(xv[c][r][e * SH + s], wt, acc[u][e]);
-                    }
+                            for (int e = 0; e < 4; ++e) acc[u][e] = fmaf(xv[c][r][e * SH + s], wt, acc[u][e]);
+                        }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + kk + u;
+                if (k < a.K) f32s_store4<ACT>(a, y, n, k, p, q0, acc[u], bias);
             }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = k0 + kk + u;
-            if (k < a.K) f32s_store4(a, y, n, k, p, q0, acc[u], bias, ep);
-        }
-    }
+    };
+    if (epi == 0)
+        body(std::integral_constant<int, -1>{});
+    else
+        with_act(a.act, [&](auto A) __attribute__((always_inline)) { body(A); });
 }
 
-// Pointwise 1x1 fp32 GEMM on v_mfma_f32_16x16x4_f32: wave = 16 pixels x KT tiles of 16
-// output channels; per MFMA a lane holds one x value (pixel l & 15, channel 4 j + (l >> 4)) and
-// one weight (output channel l & 15 of the tile, same channel): exact products, fp32 sums.
-template <int KT>
+// Pointwise 1x1 fp32 GEMM on v_mfma_f32_16x16x4_f32: wave = MI groups of 16 pixels x KT tiles of
+// 16 output channels; per MFMA a lane holds one x value (pixel l & 15, channel 4 j + (l >> 4)) and
+// one weight (output channel l & 15 of the tile, same channel): exact products, fp32 sums.  Every
+// weight a wave loads feeds MI MFMAs: a large 1x1 over few pixels (MobileNetV2's last conv,
+// 320 -> 1280 over 4,096 pixels) is bound by the L2 re-reads of its weight, once per pixel group at
+// MI = 1 (1.6 MB x 256 groups).
+template <int KT, int MI = 1>
 __global__ __launch_bounds__(256) void conv_pw_f32(const float* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ bias, float* __restrict__ y, F32sArgs a,
                                                    int epi) {
     const int lane = threadIdx.x & 63;
     const int v = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (v >= a.items) return;  // wave-uniform
-    const int pg = v % a.PG, sl = v / a.PG;
+    const int PGM = (a.PG + MI - 1) / MI;  // MI-group slices
+    const int pgs = v % PGM, sl = v / PGM;
     const int kt0 = sl * KT;
     const int nkt = min(KT, a.NT - kt0);
     const int g = lane >> 4;
     const int HW = a.P * a.Q;
-    const int64_t m = (int64_t)pg * 16 + (lane & 15);
-    const bool mok = m < a.M;
-    const int n = mok ? (int)(m / HW) : 0, pp = mok ? (int)(m - (int64_t)n * HW) : 0;
-    const float* xb = x + ((int64_t)n * a.C + g) * HW + pp;
+    const float* xb[MI];
+    bool mok[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+        const int64_t m = ((int64_t)pgs * MI + mi) * 16 + (lane & 15);
+        mok[mi] = m < a.M;
+        const int n = mok[mi] ? (int)(m / HW) : 0, pp = mok[mi] ? (int)(m - (int64_t)n * HW) : 0;
+        xb[mi] = x + ((int64_t)n * a.C + g) * HW + pp;
+    }
     const float* wb[KT];
     bool kok[KT];
 #pragma unroll
@@ -160,17 +182,20 @@ __global__ __launch_bounds__(256) void conv_pw_f32(const float* __restrict__ x, 
         kok[t] = t < nkt && k < a.K;
         wb[t] = w + (int64_t)(kok[t] ? k : 0) * a.C + g;
     }
-    floatx4 acc[KT];
+    floatx4 acc[MI][KT];
 #pragma unroll
-    for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) acc[mi][t] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int nj = (a.C + 3) / 4;
     for (int j0 = 0; j0 < nj; j0 += 4) {
-        float xa[4], wv[4][KT];
+        float xa[4][MI], wv[4][KT];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int c = 4 * (j0 + u) + g;
             const bool cok = c < a.C;
-            xa[u] = (mok && cok) ? xb[(int64_t)4 * (j0 + u) * HW] : 0.0f;
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi) xa[u][mi] = (mok[mi] && cok) ? xb[mi][(int64_t)4 * (j0 + u) * HW] : 0.0f;
 #pragma unroll
             for (int t = 0; t < KT; ++t) wv[u][t] = (kok[t] && cok) ? wb[t][4 * (j0 + u)] : 0.0f;
         }
@@ -179,33 +204,38 @@ __global__ __launch_bounds__(256) void conv_pw_f32(const float* __restrict__ x, 
             if (j0 + u >= nj) break;  // wave-uniform
 #pragma unroll
             for (int t = 0; t < KT; ++t)
-                if (t < nkt) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u], wv[u][t], acc[t], 0, 0, 0);
+#pragma unroll
+                for (int mi = 0; mi < MI; ++mi)
+                    if (t < nkt) acc[mi][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u][mi], wv[u][t], acc[mi][t], 0, 0, 0);
         }
     }
     // epilogue: lane holds D[pixel 4 g + e][channel lane & 15]
-    const int64_t mo = (int64_t)pg * 16 + 4 * g;
     const bool ep = epi != 0;
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        if (t >= nkt) break;
-        const int k = 16 * (kt0 + t) + (lane & 15);
-        if (k >= a.K) continue;
-        const float bk = bias ? bias[k] : 0.0f;
-        const float s = (ep && a.ps) ? a.ps[k] : 1.0f;
-        const float sh = (ep && a.pb) ? a.pb[k] : 0.0f;
+    for (int mi = 0; mi < MI; ++mi) {
+        const int64_t mo = ((int64_t)pgs * MI + mi) * 16 + 4 * g;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int64_t me = mo + e;
-            if (me >= a.M) break;
-            const int ne = (int)(me / HW), pe = (int)(me - (int64_t)ne * HW);
-            const int64_t off = ((int64_t)ne * a.K + k) * HW + pe;
-            float u = acc[t][e] + bk;
-            if (ep) {
-                u = u * s + sh;
-                if (a.res) u += a.res[off];
-                u = epi_act(u, a.act);
+        for (int t = 0; t < KT; ++t) {
+            if (t >= nkt) break;
+            const int k = 16 * (kt0 + t) + (lane & 15);
+            if (k >= a.K) continue;
+            const float bk = bias ? bias[k] : 0.0f;
+            const float s = (ep && a.ps) ? a.ps[k] : 1.0f;
+            const float sh = (ep && a.pb) ? a.pb[k] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t me = mo + e;
+                if (me >= a.M) break;
+                const int ne = (int)(me / HW), pe = (int)(me - (int64_t)ne * HW);
+                const int64_t off = ((int64_t)ne * a.K + k) * HW + pe;
+                float u = acc[mi][t][e] + bk;
+                if (ep) {
+                    u = u * s + sh;
+                    if (a.res) u += a.res[off];
+                    u = epi_act(u, a.act);
+                }
+                y[off] = u;
             }
-            y[off] = u;
         }
     }
 }
@@ -234,28 +264,35 @@ void f32s_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
         p.NJ = base.C <= 3 ? 3 : 4;
         const int64_t items = (int64_t)base.N * base.P * ((base.Q + 3) / 4);
         p.blocks = (items + 255) / 256;
-        PlanCand c;
-        c.plan = p;
-        c.cost = 0.0;
-        out.push_back(c);
+        for (int kb : {16, 4}) {  // plan field MI: output channels per thread
+            p.MI = kb;
+            PlanCand c;
+            c.plan = p;
+            c.cost = kb == 16 ? (items >= 65536 ? 0.0 : 1.0) : (items >= 65536 ? 1.0 : 0.0);
+            out.push_back(c);
+        }
     }
     if (base.R == 1 && base.S == 1 && base.sh == 1 && base.sw == 1 && base.ph == 0 && base.pw == 0) {
         const int NT = (base.K + 15) / 16;
         const int64_t M = (int64_t)base.N * base.P * base.Q, PG = (M + 15) / 16;
-        for (int kt : {4, 8, 2}) {
-            ConvPlan p = base;
-            common(p);
-            p.kind = KIND_PW_F32;
-            p.vrx = 0;
-            p.NJ = kt;
-            p.NT = NT;
-            const int64_t items = PG * ((NT + kt - 1) / kt);
-            if (items > (int64_t)INT32_MAX - 4) continue;
-            p.blocks = (items + 3) / 4;
-            PlanCand c;
-            c.plan = p;
-            c.cost = 1.0 + kt;
-            out.push_back(c);
+        for (int mi : {1, 2, 4}) {  // plan field MI: 16-pixel groups per wave (weight reuse)
+            for (int kt : {4, 8, 2}) {
+                if (mi > 1 && (kt == 8 || PG < 64 * mi)) continue;
+                ConvPlan p = base;
+                common(p);
+                p.kind = KIND_PW_F32;
+                p.vrx = 0;
+                p.NJ = kt;
+                p.NT = NT;
+                p.MI = mi;
+                const int64_t items = (PG + mi - 1) / mi * ((NT + kt - 1) / kt);
+                if (items > (int64_t)INT32_MAX - 4) continue;
+                p.blocks = (items + 3) / 4;
+                PlanCand c;
+                c.plan = p;
+                c.cost = 1.0 + kt + 0.5 * (mi - 1);
+                out.push_back(c);
+            }
         }
     }
 }
@@ -270,9 +307,18 @@ hipError_t launch_conv_f32s(const ConvPlan& p, const float* x, const float* w, c
     if (p.kind == KIND_DIRECT_F32) {
         a.Q4 = (p.Q + 3) / 4;
         a.items = p.N * p.P * a.Q4;
-        a.KB = 16;
-        const dim3 grid((unsigned)((a.items + 255) / 256), (unsigned)((p.K + 15) / 16)), block(256);
-        if (p.vrx == 1 && p.NJ == 3)
+        a.KB = p.MI == 4 ? 4 : 16;
+        const dim3 grid((unsigned)((a.items + 255) / 256), (unsigned)((p.K + a.KB - 1) / a.KB)), block(256);
+        if (a.KB == 4) {
+            if (p.vrx == 1 && p.NJ == 3)
+                hipLaunchKernelGGL((conv_direct_f32<1, 3, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+            else if (p.vrx == 1)
+                hipLaunchKernelGGL((conv_direct_f32<1, 4, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+            else if (p.NJ == 3)
+                hipLaunchKernelGGL((conv_direct_f32<2, 3, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+            else
+                hipLaunchKernelGGL((conv_direct_f32<2, 4, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+        } else if (p.vrx == 1 && p.NJ == 3)
             hipLaunchKernelGGL((conv_direct_f32<1, 3>), grid, block, 0, s, x, w, bias, y, a, epi);
         else if (p.vrx == 1)
             hipLaunchKernelGGL((conv_direct_f32<1, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
@@ -285,12 +331,17 @@ hipError_t launch_conv_f32s(const ConvPlan& p, const float* x, const float* w, c
     if (p.kind == KIND_PW_F32) {
         a.NT = (p.K + 15) / 16;
         a.PG = (int)((a.M + 15) / 16);
-        a.items = a.PG * ((a.NT + p.NJ - 1) / p.NJ);
+        const int mi = p.MI > 1 ? p.MI : 1;
+        a.items = (a.PG + mi - 1) / mi * ((a.NT + p.NJ - 1) / p.NJ);
         const dim3 grid((unsigned)((a.items + 3) / 4)), block(256);
-        switch (p.NJ) {
-            case 2: hipLaunchKernelGGL((conv_pw_f32<2>), grid, block, 0, s, x, w, bias, y, a, epi); break;
-            case 4: hipLaunchKernelGGL((conv_pw_f32<4>), grid, block, 0, s, x, w, bias, y, a, epi); break;
-            case 8: hipLaunchKernelGGL((conv_pw_f32<8>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+        switch (p.NJ * 10 + mi) {
+            case 21: hipLaunchKernelGGL((conv_pw_f32<2>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 41: hipLaunchKernelGGL((conv_pw_f32<4>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 81: hipLaunchKernelGGL((conv_pw_f32<8>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 22: hipLaunchKernelGGL((conv_pw_f32<2, 2>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 42: hipLaunchKernelGGL((conv_pw_f32<4, 2>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 24: hipLaunchKernelGGL((conv_pw_f32<2, 4>), grid, block, 0, s, x, w, bias, y, a, epi); break;
+            case 44: hipLaunchKernelGGL((conv_pw_f32<4, 4>), grid, block, 0, s, x, w, bias, y, a, epi); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

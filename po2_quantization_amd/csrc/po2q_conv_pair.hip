@@ -173,7 +173,15 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nw = (int)(blockDim.x >> 6) - MW;  // compute waves (MW: wave nw is the memory wave)
-    const int rawslot = CC * a.Wp * 4;
+    // bytes per channel row of the raw x ring.  MW at C = 16 pads each row by one float4: the row pitch is then
+    // 4 dwords off a multiple of 32 banks, so the halo reads (one column, 8 / 16 channels per 32-lane
+    // group) hit distinct banks instead of one (16-way at C = 16: SQ_LDS_BANK_CONFLICT)
+    // (C = 16 only: at C = 32 the padded ring would not leave 5 slots in the LDS)
+    constexpr bool RPAD = MW && CC == 16;
+    const int RPB = a.Wp * 4 + (RPAD ? 16 : 0);
+    // padded: a slot is whole 1 KiB DMA instructions (the last one's tail lanes load zeros past the
+    // padded rows; they must land inside the slot)
+    const int rawslot = RPAD ? (CC * RPB + 1023) / 1024 * 1024 : CC * RPB;
     // the intermediate planes are sized for the widest image (7 waves): a compile-time pitch turns
     // every slot / plane offset of the fragment reads and epilogue writes into an immediate
     constexpr int YPL = (7 * SW + 3) * 2 * CC;
@@ -245,15 +253,16 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     // (side, channel) from the neighbours' columns of the shared raw row (zero outside)
     const int sc = lane % SW, so = lane / SW;
     const int wa_i = xa<CC>(sc + 1, so);
-    // (lanes 2C.. -- C = 16 -- repeat lanes 0 .. 2C-1: they read and write the same halo values,
-    // so the halo split needs no divergent branch)
-    const int hl = lane % (2 * CC);
-    const int hside = (hl / CC) & 1, hch = hl % CC;
+    // Each 32-lane group (one LDS cycle of ds_read_b32) reads C / 2 channels of both halo columns:
+    // group g takes channels (C / 2) g .. + C / 2 - 1, its lane l -> side (l % C) / (C / 2); at C = 16
+    // lanes 16-31 of a group repeat lanes 0-15 (same values to the same addresses: no divergent branch)
+    const int hl = lane % CC;
+    const int hside = hl / (CC / 2), hch = (CC / 2) * (lane >> 5) + hl % (CC / 2);
     const int hq = hside ? q0 + SW : q0 - 1;
     const bool h_ok = hq >= 0 && hq < a.W;
     const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
-    const int rdx0 = (so * 8) * (a.Wp * 4) + (q0 + sc) * 4;
-    const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
+    const int rdx0 = (so * 8) * RPB + (q0 + sc) * 4;
+    const int rdx_h = hch * RPB + (h_ok ? hq : 0) * 4;
     // A fragment addresses: x planes (wave-private, pixel = strip column + 1) and shared
     // intermediate planes (pixel = column + 1, swizzled octet o): one b128 each
     // C = 16 pairs the s2 tap of two planes in one k-step: per halo row and group the k-steps are
@@ -319,16 +328,30 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     // 3 tap rows x KS k-steps x 3 planes x NG groups x NT tiles of MFMAs on one split row
     // into accumulator slots SL.  TR (conv 1): transposed (A = weights), x planes, VGPR
     // weights; else (conv 2): shared planes (two b64 per fragment), weights per WL2
+    // PF (conv 2, -DPO2Q_PAIR_PF=1; off): the fragments of k-step ks + 1 (A from the shared planes; B
+    // from LDS at C = 32) read before the MFMAs of k-step ks, into a second register set, pinned there
+    // by a sched_barrier (the compiler issues each read one or two MFMA groups before its use).  Waits
+    // per C = 32 step 33 -> 22 and the conv-2 phase 2402 -> 2186 cycles in the stamps build, but the
+    // product kernels did not get faster: C = 32 plain 0.362 vs 0.351 ms, and the C = 32 BasicBlock
+    // form ran out of VGPRs (0.637 vs 0.380 ms), same box (profiles/r05_pair_pf_ab.jsonl).  The conv-2
+    // phase is long because it is the phase right after the barrier, where both waves of a SIMD issue
+    // MFMAs at once (2 x 54 x 16 cycles), not because of the read latency.
+#ifndef PO2Q_PAIR_PF
+#define PO2Q_PAIR_PF 0
+#endif
+    // 3 tap rows x KS k-steps x 3 planes x NG groups x NT tiles of MFMAs on one split row
+    // into accumulator slots SL.  TR (conv 1): transposed (A = weights), x planes, VGPR
+    // weights; else (conv 2): shared planes (two b64 per fragment), weights per WL2
     auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG][NT], const bf16x8 (&bw)[NF],
                      const bf16x8 (&bw2v)[WL2 ? 1 : NF], const unsigned char* pb) __attribute__((always_inline)) {
         constexpr int SR = decltype(S_)::value;
         constexpr bool TR = decltype(TR_)::value;
+        constexpr bool PF = !TR && PO2Q_PAIR_PF != 0;
         constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            // fragments of this k-step: the 3 planes, or for C = 16's k-step 1 the two paired ones
+        // fragments of k-step ks: the 3 planes, or for C = 16's k-step 1 the two paired ones; at
+        // C = 32 (conv 2) also the 3 x NT B fragments of the k-step from LDS
+        auto load_a = [&](int ks, bf16x8 (&af)[3][NG]) __attribute__((always_inline)) {
             const int np = (CC == 16 && ks == 1) ? 2 : 3;
-            bf16x8 af[3][NG];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
@@ -341,6 +364,26 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                         off = TR ? pl * PL + aoff[grp][ks] : pl * YPL + yoff[grp][ks];
                     af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + off));
                 }
+        };
+        auto load_b = [&](int ks, bf16x8 (&bf)[3][NT]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int r3 = 0; r3 < 3; ++r3)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int rr = 2 - r3;
+                    const int f = (rr * KS + ks) * NT + nt;
+                    if constexpr (TR)
+                        bf[r3][nt] = bw[f];
+                    else if (WL2 && W2R && rr == 0)
+                        bf[r3][nt] = bw2r[W2R ? f : 0];
+                    else if constexpr (WL2)
+                        bf[r3][nt] = __builtin_bit_cast(bf16x8, wl2[f * 64 + lane]);
+                    else
+                        bf[r3][nt] = bw2v[WL2 ? 0 : f];
+                }
+        };
+        auto mma = [&](int ks, const bf16x8 (&af)[3][NG], const bf16x8 (&bf)[3][NT]) __attribute__((always_inline)) {
+            const int np = (CC == 16 && ks == 1) ? 2 : 3;
             // tap row 2 first: it feeds the slot that completes this step, so its epilogue can
             // start while the other tap rows' MFMAs of the last k-step still run
 #pragma unroll
@@ -348,16 +391,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     const int rr = 2 - r3;
-                    const int f = (rr * KS + ks) * NT + nt;
-                    bf16x8 b;
-                    if constexpr (TR)
-                        b = bw[f];
-                    else if (WL2 && W2R && rr == 0)
-                        b = bw2r[W2R ? f : 0];
-                    else if constexpr (WL2)
-                        b = __builtin_bit_cast(bf16x8, wl2[f * 64 + lane]);
-                    else
-                        b = bw2v[WL2 ? 0 : f];
+                    const bf16x8 b = bf[r3][nt];
 #pragma unroll
                     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
@@ -371,6 +405,30 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                                                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, c, 0, 0, 0);
                         }
                 }
+        };
+        if constexpr (PF) {
+            bf16x8 af[2][3][NG], bf[2][3][NT];
+            load_a(0, af[0]);
+            load_b(0, bf[0]);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                if (ks + 1 < KS) {
+                    load_a(ks + 1, af[(ks + 1) & 1]);
+                    load_b(ks + 1, bf[(ks + 1) & 1]);
+                    // pins the reads above this k-step's MFMAs (the scheduler otherwise sinks each to
+                    // just before its use); the waits stay counted (lgkmcnt(N)) before each MFMA group
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                mma(ks, af[ks & 1], bf[ks & 1]);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                bf16x8 af[3][NG], bf[3][NT];
+                load_a(ks, af);
+                load_b(ks, bf);
+                mma(ks, af, bf);
+            }
         }
     };
 
@@ -408,7 +466,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                                         : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
                 }
                 if constexpr (RES) {
-                    const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * (a.Wp * 4) + ql * 4)
+                    const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * RPB + ql * 4)
                                          : *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] += r[e];
@@ -502,7 +560,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         {
             const unsigned char* rw = raw + RS * rawslot;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * (a.Wp * 4));
+            for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * RPB);
             hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
         }
         if constexpr (STG != 0) {
@@ -588,18 +646,23 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #endif
     };
 
-    // MW: the memory wave's DMA of x row jn into its raw ring slot: every float4 of the row's C x Wp/4
-    // (instruction i, lane l -> float4 64 i + l; the compute waves' own load_row split it 2 per wave)
+    // MW: the memory wave's DMA of x row jn into its raw ring slot: every float4 of the row's C x (Wp/4 + 1)
+    // padded layout (instruction i, lane l -> float4 64 i + l; the pad float4 of each channel row and the
+    // tail past C rows load out of range, i.e. zeros).  MWD instructions (15 where 14 covered the
+    // unpadded row; MW runs 7 compute waves only: Wp = 7 x 512 / C)
+    constexpr int MWW4 = 7 * SW / 4 + (RPAD ? 1 : 0);  // float4 per (padded) channel row
+    constexpr int MWD = (CC * MWW4 + 63) / 64;
     auto mw_row = [&](int jn) __attribute__((always_inline)) {
         const int h = p0 - 2 + jn;
         const bool hok = jn < nx && h >= 0 && h < a.H;
         const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
         const uint32_t base = raw_lds + (uint32_t)((jn % PD) * rawslot);
 #pragma unroll
-        for (int i = 0; i < 14; ++i) {
+        for (int i = 0; i < MWD; ++i) {
             const int e = 64 * i + lane;
-            const int c = e / W4, q = 4 * (e - c * W4);
-            const uint32_t vo = (hok && q < a.W) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u + roff : 0x7fffffffu;
+            const int c = e / MWW4, q = 4 * (e - c * MWW4);
+            const uint32_t vo = (hok && c < CC && q < a.W) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u + roff
+                                                            : 0x7fffffffu;
             rows_dma16<(NTS & 2) != 0>(rs, vo, 0u, base + (uint32_t)i * 1024u);
         }
     };
@@ -710,7 +773,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             // every wave finished before the barrier) takes row j + PD - 1.  Same barrier count as the
             // compute waves' loop.
             auto mstep = [&](int j) __attribute__((always_inline)) {
-                rows_wait<14 * (PD - MWL - 1)>();  // row j landed (rows j + 1 .. j + PD - MWL - 1 may fly)
+                rows_wait<MWD * (PD - MWL - 1)>();  // row j landed (rows j + 1 .. j + PD - MWL - 1 may fly)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 mw_row(j + PD - MWL);  // into the slot of row j - MWL, whose last reader was step j - 1
             };
@@ -1084,17 +1147,18 @@ struct PairPlan {
     size_t lds = 0;
 };
 
-static size_t pair_lds(int C, int waves, int pd, bool res) {  // res: the compute waves' residual slots
+static size_t pair_lds(int C, int waves, int pd, bool res, bool mw = false) {  // res: the compute waves' residual slots
     const int sw = 512 / C, wp = sw * waves;
     const int plane = (sw + 2) * 2 * C + 32;
     const int nf = 3 * (C == 16 ? 2 : 3) * (C / 16);
-    return (size_t)pd * C * wp * 4 + 2 * 3 * (size_t)(7 * sw + 3) * 2 * C + (size_t)waves * 3 * plane +
+    const size_t slot = (mw && C == 16) ? ((size_t)C * (wp * 4 + 16) + 1023) / 1024 * 1024 : (size_t)C * wp * 4;
+    return (size_t)pd * slot + 2 * 3 * (size_t)(7 * sw + 3) * 2 * C + (size_t)waves * 3 * plane +
            (res ? (size_t)waves * pd * kQResSlot : 0) + (C == 32 ? (size_t)nf * 64 * 16 : 0);
 }
 
 // One block per CU (7 waves); segments of RB output rows: the fewest segments that still
 // give every CU a block, each recomputing 2 intermediate rows of its neighbours.
-static bool pair_plan(PairPlan& pp, int N, int C, int H, int W, bool res, int pd, int nts) {
+static bool pair_plan(PairPlan& pp, int N, int C, int H, int W, bool res, int pd, int nts, bool mw = false) {
     if (N <= 0 || H <= 0 || W <= 0 || W % 4 != 0 || (C != 16 && C != 32)) return false;
     const int sw = 512 / C;
     const int waves = (W + sw - 1) / sw;
@@ -1104,7 +1168,7 @@ static bool pair_plan(PairPlan& pp, int N, int C, int H, int W, bool res, int pd
     pp.waves = waves;
     pp.pd = pd;
     pp.nts = nts;
-    pp.lds = pair_lds(C, waves, pd, res);
+    pp.lds = pair_lds(C, waves, pd, res, mw);
     if (pp.lds > 160 * 1024) return false;
     int nseg = std::max(1, (256 + N - 1) / N);
     nseg = std::min(nseg, std::max(1, H / 8));
@@ -1201,6 +1265,10 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 #endif
 #define PO2Q_PR(c, d, nt) \
     if (pp.C == c && pp.pd == d && pp.nts == nt) return launch_pair_t<c, d, nt>(pp, a, x, y, res, s);
+#ifdef PO2Q_PAIR_ISA_ONLY  // ISA inspection builds (hipcc -S): the two default plans only
+    PO2Q_PR(16, 5, 3) PO2Q_PR(32, 2, 3)
+    return hipErrorInvalidValue;
+#endif
     PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
     PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
     PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
@@ -1373,7 +1441,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
             a.mw = 1;
             pd = residual ? 6 : d;
             nts = 3;  // with the ring residual no x row is re-read from memory: non-temporal loads
-            if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, false, pd, nts)) {
+            if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, false, pd, nts, true)) {
                 po2q::set_error("po2q: pair: no memory-wave plan for this shape");
                 return PO2Q_ERR_UNSUPPORTED;
             }

@@ -43,10 +43,15 @@ struct PwArgs {
 // at 2x2 / 1x1 pixels, where 16-pixel groups are few and C is up to 960): a block = ONE item,
 // wave w takes the k-steps ks = w mod 4, and the 4 partial sums are added through LDS in a
 // fixed order (deterministic) before wave 0's epilogue -- a 4x shorter dependent load chain.
-template <int KT, bool EPI, int KSPLIT = 1>
+// PD (plan field nts + 1): k-steps whose x values and B fragments are in flight at once.  1: the next
+// k-step's loads go out before the current one's MFMAs.  3: three k-steps ahead -- the small late
+// layers are a chain of dependent load latencies (a few us per launch at 2x2 / 1x1 pixels), which a
+// deeper ring shortens 3x; more VGPRs, so the autotuner keeps PD 1 where occupancy matters.
+template <int KT, bool EPI, int KSPLIT = 1, int PD = 1>
 __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, const uint4* __restrict__ wp,
                                                const float* __restrict__ scale_p, const float* __restrict__ bias,
                                                float* __restrict__ y, PwArgs a) {
+    static_assert(PD == 1 || PD == 3, "k-step ring depth");
     const int lane = threadIdx.x & 63;
     const int wv = (int)(threadIdx.x >> 6);
     const int v = KSPLIT == 1 ? (int)blockIdx.x * 4 + wv : (int)blockIdx.x;
@@ -70,19 +75,16 @@ __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, cons
         for (int e = 0; e < 8; ++e)
             b[e] = (mok && c0 + e < a.C) ? __float_as_uint(xb[(int64_t)(32 * ks + e) * cstride]) : 0u;
     };
+    auto loadw = [&](int ks, uint4 (&bw)[KT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+            bw[t] = t < nkt ? wp[((int64_t)ks * a.NT + kt0 + t) * 64 + lane] : make_uint4(0u, 0u, 0u, 0u);
+    };
 
     floatx4 acc[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    uint32_t cur[8];
-    if (ks0 < a.KS) load8(ks0, cur);
-    for (int ks = ks0; ks < a.KS; ks += KSPLIT) {
-        uint32_t nxt[8];
-        if (ks + KSPLIT < a.KS) load8(ks + KSPLIT, nxt);
-        uint4 bw[KT];
-#pragma unroll
-        for (int t = 0; t < KT; ++t)
-            bw[t] = t < nkt ? wp[((int64_t)ks * a.NT + kt0 + t) * 64 + lane] : make_uint4(0u, 0u, 0u, 0u);
+    auto mma = [&](const uint32_t (&cur)[8], const uint4 (&bw)[KT]) __attribute__((always_inline)) {
         uint4 hi, mid, lo;
         split3(cur, hi, mid, lo);
         const bf16x8 ah = __builtin_bit_cast(bf16x8, hi), am = __builtin_bit_cast(bf16x8, mid),
@@ -96,9 +98,45 @@ __global__ __launch_bounds__(256) void conv_pw(const float* __restrict__ x, cons
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, acc[t], 0, 0, 0);
             }
         }
-        if (ks + KSPLIT < a.KS) {
+    };
+    if constexpr (PD == 1) {
+        uint32_t cur[8];
+        if (ks0 < a.KS) load8(ks0, cur);
+        for (int ks = ks0; ks < a.KS; ks += KSPLIT) {
+            uint32_t nxt[8];
+            if (ks + KSPLIT < a.KS) load8(ks + KSPLIT, nxt);
+            uint4 bw[KT];
+            loadw(ks, bw);
+            mma(cur, bw);
+            if (ks + KSPLIT < a.KS) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) cur[e] = nxt[e];
+                for (int e = 0; e < 8; ++e) cur[e] = nxt[e];
+            }
+        }
+    } else {
+        // a 3-slot ring (compile-time slots: the loop is unrolled by 3); the guards are wave-uniform
+        uint32_t xr[3][8];
+        uint4 wr[3][KT];
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+            const int ks = ks0 + s3 * KSPLIT;
+            if (ks < a.KS) {
+                load8(ks, xr[s3]);
+                loadw(ks, wr[s3]);
+            }
+        }
+        for (int ks = ks0; ks < a.KS; ks += 3 * KSPLIT) {
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3) {
+                const int kc = ks + s3 * KSPLIT;
+                if (kc >= a.KS) break;
+                mma(xr[s3], wr[s3]);
+                const int kn = kc + 3 * KSPLIT;
+                if (kn < a.KS) {
+                    load8(kn, xr[s3]);
+                    loadw(kn, wr[s3]);
+                }
+            }
         }
     }
     if constexpr (KSPLIT > 1) {
@@ -213,18 +251,26 @@ void pw_candidates(const ConvPlan& base, int mode, int bits, int fsr, std::vecto
     const int KS = (base.C + 31) / 32;
     for (int ksplit : {1, 4}) {
         for (int kt : {2, 4, 8}) {
-            if (kt > 2 && (NT + kt / 2 - 1) / (kt / 2) <= 1) continue;  // no wider than the channel count needs
-            if (ksplit > 1 && KS < 2 * ksplit) continue;                 // too few k-steps to split
-            ConvPlan p = base;
-            if (!pw_plan_one(p, kt, ksplit)) continue;
-            // cost: the dependent k-step chain of a wave, scaled up when too few waves fill the chip
-            const int64_t waves = PG * ((NT + kt - 1) / kt) * ksplit;
-            const double fill = std::min(1.0, (double)waves / 4096.0);
-            const double chain = ((KS + ksplit - 1) / ksplit) * (24.0 + 3.0 * 16.0 * std::min(kt, NT) / 8.0) + 40.0;
-            PlanCand c;
-            c.plan = p;
-            c.cost = (double)waves * chain / ksplit / fill + (fill < 1.0 ? chain * 64.0 : 0.0);
-            out.push_back(c);
+            for (int pd : {1, 3}) {
+                if (kt > 2 && (NT + kt / 2 - 1) / (kt / 2) <= 1) continue;  // no wider than the channel count needs
+                if (ksplit > 1 && KS < 2 * ksplit) continue;                 // too few k-steps to split
+                const int steps = (KS + ksplit - 1) / ksplit;                // k-steps of one wave's chain
+                if (pd > 1 && (steps < 3 || kt > 4)) continue;                // a ring deeper than the chain / VGPRs
+                ConvPlan p = base;
+                if (!pw_plan_one(p, kt, ksplit)) continue;
+                p.nts = pd - 1;
+                // cost: the dependent k-step chain of a wave (a load latency per k-step, or per pd
+                // k-steps with the ring), scaled up when too few waves fill the chip; the ring's VGPRs
+                // cost occupancy where the chip is full
+                const int64_t waves = PG * ((NT + kt - 1) / kt) * ksplit;
+                const double fill = std::min(1.0, (double)waves / 4096.0);
+                const double chain = steps * (24.0 / pd + 3.0 * 16.0 * std::min(kt, NT) / 8.0) + 40.0;
+                PlanCand c;
+                c.plan = p;
+                c.cost = (double)waves * chain / ksplit / fill * (pd > 1 && fill >= 1.0 ? 1.5 : 1.0) +
+                         (fill < 1.0 ? chain * 64.0 : 0.0);
+                out.push_back(c);
+            }
         }
     }
     std::stable_sort(out.begin(), out.end(), [](const PlanCand& u, const PlanCand& v) { return u.cost < v.cost; });
@@ -234,6 +280,21 @@ template <int KT>
 static hipError_t launch_pw_t(const ConvPlan& p, const PwArgs& a, const float* x, const uint4* wp, const float* scale,
                               const float* bias, float* y, bool epi, hipStream_t s) {
     const dim3 grid((unsigned)p.blocks), block(256);
+    if constexpr (KT <= 4) {
+        if (p.nts == 2) {  // the 3-deep k-step ring
+            if (p.pd == 4) {
+                if (epi)
+                    hipLaunchKernelGGL((conv_pw<KT, true, 4, 3>), grid, block, 0, s, x, wp, scale, bias, y, a);
+                else
+                    hipLaunchKernelGGL((conv_pw<KT, false, 4, 3>), grid, block, 0, s, x, wp, scale, bias, y, a);
+            } else if (epi) {
+                hipLaunchKernelGGL((conv_pw<KT, true, 1, 3>), grid, block, 0, s, x, wp, scale, bias, y, a);
+            } else {
+                hipLaunchKernelGGL((conv_pw<KT, false, 1, 3>), grid, block, 0, s, x, wp, scale, bias, y, a);
+            }
+            return hipGetLastError();
+        }
+    }
     if (p.pd == 4) {
         if (epi)
             hipLaunchKernelGGL((conv_pw<KT, true, 4>), grid, block, 0, s, x, wp, scale, bias, y, a);

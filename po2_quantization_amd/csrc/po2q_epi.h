@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "po2q_internal.h"
 
 namespace po2q {
@@ -23,6 +25,26 @@ __device__ __forceinline__ float epi_act(float v, int act) {
     if (act == 2) return v <= 0.0f ? 0.0f : (v >= 6.0f ? 6.0f : v);         // relu6 = hardtanh(0, 6)
     if (act == 3) return v / (1.0f + expf(-v));                              // silu
     return v;
+}
+
+// epi_act with the activation a compile-time constant: no per-value branch on a runtime act (a
+// kernel dispatches its whole epilogue once per layer / launch instead).
+template <int ACT>
+__device__ __forceinline__ float epi_act_ct(float v) {
+    static_assert(ACT >= 0 && ACT <= 3, "activation");
+    return epi_act(v, ACT);
+}
+
+// Calls f(std::integral_constant<int, ACT>{}) for a runtime act in 0..3 (wave-uniform: one scalar
+// branch per call site).
+template <class F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
+    switch (act) {
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        default: f(std::integral_constant<int, 0>{}); break;
+    }
 }
 
 // Row-streaming kernels with the affine map + activation in their store epilogue

@@ -161,6 +161,7 @@ struct PackReq {
     void* packed;
     float* scale;
     int bits, fsr, mode;
+    unsigned* partial = nullptr;  // absmax_blocks(n) words of the plan's workspace (null: fused absmax only)
 };
 // whether a plan's weight staging can join a batched pack (quantized, fused absmax size,
 // bf16x3 or depthwise kind)

@@ -302,8 +302,9 @@ struct PackJob {
     const float* w;
     void* packed;
     float* scale;
+    const unsigned* partial;  // nparts > 0: max|w| from these absmax partials (absmax_batch_kernel)
     int64_t n;
-    int lo, hi, mode, nb, plain;
+    int lo, hi, mode, nb, plain, nparts;
     PackX3 pg;
 };
 constexpr int kPackBatch = 24;  // 24 x 104-byte jobs: 2.5 KB of kernel arguments
@@ -311,20 +312,67 @@ struct PackBatch {
     PackJob job[kPackBatch];
 };
 
+// The absmax of the batch's larger tensors as its own launch in front of pack_batch_kernel: block
+// (c, layer) reduces chunk c (kAbsChunk elements: one float4 per thread x 4 in flight) into
+// partial[c] of the layer's workspace.  Without it every pack block of a layer re-reads the whole
+// tensor for the scale (up to 32 blocks x 1.2 MB per MobileNetV2 1x1 layer: ~20 us per batch launch,
+// profiles/r04_mobilenet32_kernel_stats.csv); max is order-free, so the result is the same bits.
+constexpr int kAbsChunk = 4 * 256 * 4;  // = absmax_blocks' elements per partial
+struct AbsJob {
+    const float* w;
+    unsigned* partial;
+    int64_t n;
+    int nparts;
+};
+struct AbsBatch {
+    AbsJob job[kPackBatch];
+};
+__global__ __launch_bounds__(256) void absmax_batch_kernel(AbsBatch B) {
+    const AbsJob& j = B.job[blockIdx.y];
+    if ((int)blockIdx.x >= j.nparts) return;  // block-uniform
+    __shared__ unsigned red4[4];
+    const int64_t c0 = (int64_t)blockIdx.x * kAbsChunk;
+    const int64_t c1 = min(j.n, c0 + kAbsChunk);
+    unsigned m = 0u;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(j.w) & 15u) == 0);
+    if (aligned && c1 - c0 == kAbsChunk) {
+        const float4* w4 = reinterpret_cast<const float4*>(j.w + c0);
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = w4[u * 256 + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const unsigned a = __float_as_uint(v[u].x) & 0x7fffffffu, b = __float_as_uint(v[u].y) & 0x7fffffffu;
+            const unsigned c = __float_as_uint(v[u].z) & 0x7fffffffu, d = __float_as_uint(v[u].w) & 0x7fffffffu;
+            m = max(m, max(max(a, b), max(c, d)));
+        }
+    } else {
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) m = max(m, __float_as_uint(j.w[i]) & 0x7fffffffu);
+    }
+    m = block_max_u32(m, red4);
+    if (threadIdx.x == 0) j.partial[blockIdx.x] = m;
+}
+
 __global__ __launch_bounds__(kPackThreads) void pack_batch_kernel(PackBatch B) {
     const PackJob& j = B.job[blockIdx.y];
     if ((int)blockIdx.x >= j.nb) return;  // block-uniform
     if (j.plain) {
         __shared__ unsigned red[kPackThreads / 64];
-        const unsigned m = block_max_u32<kPackThreads / 64>(fused_absmax_bits(j.w, j.n), red);
+        unsigned m0 = 0u;
+        if (j.nparts > 0) {
+            for (int i = threadIdx.x; i < j.nparts; i += kPackThreads) m0 = max(m0, j.partial[i]);
+        } else {
+            m0 = fused_absmax_bits(j.w, j.n);
+        }
+        const unsigned m = block_max_u32<kPackThreads / 64>(m0, red);
         const float scale = __uint_as_float(m);
         float* out = reinterpret_cast<float*>(j.packed);
         for (int i = blockIdx.x * kPackThreads + threadIdx.x; i < (int)j.n; i += j.nb * kPackThreads)
             out[i] = quantize_elem(j.w[i], scale, j.mode, j.lo, j.hi);
         return;
     }
-    pack_bf16x3_body(j.w, j.n, nullptr, 0, j.lo, j.hi, j.mode, j.pg, reinterpret_cast<uint16_t*>(j.packed), j.scale,
-                     (int)blockIdx.x, j.nb);
+    pack_bf16x3_body(j.w, j.n, j.partial, j.nparts, j.lo, j.hi, j.mode, j.pg, reinterpret_cast<uint16_t*>(j.packed),
+                     j.scale, (int)blockIdx.x, j.nb);
 }
 
 static PackX3 pack_geom(const ConvPlan& p) {
@@ -347,11 +395,16 @@ bool pack_batchable(const ConvPlan& p, int mode) {
     return is_bf16x3_kind(p.kind) || p.kind == KIND_DEPTHWISE;
 }
 
+// tensors above this many weights get their absmax from absmax_batch_kernel (a pack block would
+// otherwise re-read more than this per block for the scale)
+constexpr int64_t kTwoPhaseAbsmax = 16384;
+
 hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s) {
     for (int i0 = 0; i0 < n; i0 += kPackBatch) {
         PackBatch B;
+        AbsBatch A;
         const int m = std::min(kPackBatch, n - i0);
-        int nbmax = 1;
+        int nbmax = 1, npmax = 0;
         for (int i = 0; i < m; ++i) {
             const PackReq& r = reqs[i0 + i];
             const ConvPlan& p = *r.plan;
@@ -362,6 +415,10 @@ hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s) {
             j.packed = r.packed;
             j.scale = r.scale;
             j.n = (int64_t)p.K * p.Cg * p.R * p.S;
+            j.nparts = (r.partial && j.n > kTwoPhaseAbsmax) ? (int)((j.n + kAbsChunk - 1) / kAbsChunk) : 0;
+            j.partial = r.partial;
+            A.job[i] = AbsJob{r.w, r.partial, j.n, j.nparts};
+            npmax = std::max(npmax, j.nparts);
             j.lo = lo; j.hi = hi; j.mode = r.mode - 1;
             j.plain = p.kind == KIND_DEPTHWISE ? 1 : 0;
             if (j.plain) {
@@ -372,6 +429,11 @@ hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s) {
                 j.nb = pack_blocks(j.pg);
             }
             nbmax = std::max(nbmax, j.nb);
+        }
+        if (npmax > 0) {
+            hipLaunchKernelGGL(absmax_batch_kernel, dim3((unsigned)npmax, (unsigned)m), dim3(256), 0, s, A);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(pack_batch_kernel, dim3((unsigned)nbmax, (unsigned)m), dim3(kPackThreads), 0, s, B);
         const hipError_t e = hipGetLastError();

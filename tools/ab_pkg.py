@@ -6,6 +6,7 @@ tools/make_ab_old.sh, so both libraries travel to the GPU box; delete it when do
   python tools/ab_pkg.py pair      # conv_pair stage 1 (bs = 256 @224): plain chain and BasicBlock form
   python tools/ab_pkg.py bench     # bench.py's chain (no CPU baseline / extra configs)
   python tools/ab_pkg.py cifar     # bench.py's config-2 line (ResNet56 @32 chain kernels, HIP graph)
+  python tools/ab_pkg.py models    # bench.py's config-3 / config-5 lines (MobileNetV2 @32, MobileViT @256)
   python tools/ab_pkg.py bench 3 PO2Q_PAIR_C32=1   # the working tree without / with an env setting
 """
 import json
@@ -52,6 +53,8 @@ def run_arm(root, what, extra=None):
         cmd = [sys.executable, "-c", PAIR]
     elif what == "cifar":  # the config-2 chain (ResNet56 @32, HIP graph) of bench.py's extra line
         cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-models"]
+    elif what == "models":  # the config-3 / config-5 lines (MobileNetV2 @32, MobileViT-XS @256, HIP graphs)
+        cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-cifar"]
     else:
         cmd = [sys.executable, "bench.py", "--steps", "30", "--warmup", "3", "--no-cpu-baseline", "--no-cifar",
                "--no-models"]
@@ -67,6 +70,8 @@ def run_arm(root, what, extra=None):
                 c = d["config2_cifar32"]
                 return {"img_s": c["value"], "ms_per_step": c["ms_per_step"],
                         "chain16_ms": c["roofline"]["avg_launch_ms"]}
+            if what == "models":
+                return {"c3_img_s": d["config3_mobilenet32"]["value"], "c5_img_s": d["config5_mobilevit256"]["value"]}
             return {"img_s": d["value"], "ms_per_step": d["ms_per_step"]}
     raise RuntimeError("no result from " + root)
 
