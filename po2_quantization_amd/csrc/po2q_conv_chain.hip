@@ -45,6 +45,7 @@ namespace po2q {
 
 namespace {
 constexpr int kChainThreads = 512;  // 8 waves: two per SIMD
+constexpr int kChainItems = 5;      // split items (pixel x channel octet) per thread and load batch
 constexpr int kChainMax = PO2Q_CHAIN_MAX_LAYERS;
 constexpr size_t kChainLdsMax = 160 * 1024;
 
@@ -167,62 +168,32 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     const float* xn = x + (int64_t)n * img;
     float* yn = y + (int64_t)n * img;
 
-    // ---- x -> split planes (written once: later layers write interiors).  A lane takes 4 consecutive
-    // pixels x 8 channels: 8 float4 loads (where one pixel per lane took 8 scattered dword loads per
-    // 8 values), then the split of each pixel's 8 channels into its octet of the 3 planes.  The
-    // zero halo (padded rows 0 / H + 1, columns 0 / W + 1) is written by a pass of its own.
-    {
-        const int W4 = W >> 2;
-        const int nq = H * W4 * NO;  // interior quads x channel octets (W % 4 == 0, host-checked)
-        const bool xaligned = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;  // block-uniform
-        for (int it = tid; it < nq; it += kChainThreads) {
-            const int q4 = it % W4, t = it / W4;
-            const int h = t % H, oc = t / H;
-            const float* src = xn + (int64_t)(8 * oc) * HW + h * W + 4 * q4;
-            float4 v4[8];
-            if (xaligned) {
+    // ---- x -> split planes, the zero halo with it (written once: later layers write interiors)
+    const int nitems = (H + 2) * PW * NO;
+    for (int base = 0; base < nitems; base += kChainThreads * kChainItems) {
+        uint32_t v[kChainItems][8];
+        int dst[kChainItems];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v4[e] = *reinterpret_cast<const float4*>(src + (int64_t)e * HW);
-            } else {  // an input view that is not 16-byte aligned: dword loads
+        for (int i = 0; i < kChainItems; ++i) {
+            const int it = base + i * kChainThreads + tid;
+            const bool ok = it < nitems;
+            const int pc = it % PW, t = it / PW;
+            const int rr = t % (H + 2), oc = t / (H + 2);
+            const int h = rr - 1, xc = pc - 1;
+            const bool inb = ok && h >= 0 && h < H && xc >= 0 && xc < W;
+            const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float* r = src + (int64_t)e * HW;
-                    v4[e] = make_float4(r[0], r[1], r[2], r[3]);
-                }
-            }
-#pragma unroll
-            for (int px = 0; px < 4; ++px) {
-                uint32_t v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    v[e] = __float_as_uint(px == 0 ? v4[e].x : px == 1 ? v4[e].y : px == 2 ? v4[e].z : v4[e].w);
-                const int pc = 4 * q4 + px + 1;
-                const int dst = ch_addr<C, W8, S16>((h + 1) * PW + pc, pc, oc);
-                uint4 hi, mid, lo;
-                split3(v, hi, mid, lo);
-                *reinterpret_cast<uint4*>(lds + dst) = hi;
-                *reinterpret_cast<uint4*>(lds + a.PL + dst) = mid;
-                *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst) = lo;
-            }
+            for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
+            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc) : -1;
         }
-        // the zero halo: rows 0 and H + 1 (every padded column), columns 0 and W + 1 (rows 1 .. H)
-        const int nb = (2 * PW + 2 * H) * NO;
-        for (int it = tid; it < nb; it += kChainThreads) {
-            const int oc = it % NO, b = it / NO;
-            int rr, pc;
-            if (b < 2 * PW) {
-                rr = b < PW ? 0 : H + 1;
-                pc = b < PW ? b : b - PW;
-            } else {
-                const int k = b - 2 * PW;
-                rr = 1 + (k >> 1);
-                pc = (k & 1) ? W + 1 : 0;
-            }
-            const int dst = ch_addr<C, W8, S16>(rr * PW + pc, pc, oc);
-            const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-            *reinterpret_cast<uint4*>(lds + dst) = z;
-            *reinterpret_cast<uint4*>(lds + a.PL + dst) = z;
-            *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst) = z;
+#pragma unroll
+        for (int i = 0; i < kChainItems; ++i) {
+            if (dst[i] < 0) continue;
+            uint4 hi, mid, lo;
+            split3(v[i], hi, mid, lo);
+            *reinterpret_cast<uint4*>(lds + dst[i]) = hi;
+            *reinterpret_cast<uint4*>(lds + a.PL + dst[i]) = mid;
+            *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst[i]) = lo;
         }
     }
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.PL + a.ZO) = make_uint4(0u, 0u, 0u, 0u);
