@@ -132,3 +132,40 @@ def test_session_ignores_modules_of_other_models():
             yb = b(x)  # b's layers are not a's: no recording, no pack lookups
         assert sess.recording == []
         assert torch.equal(yb, ref_b)
+
+
+@pytest.mark.parametrize("name,image", [("mobilenet", 32), ("mobilevit", 64)])
+def test_side_stream_packs_ordered_and_graph_capturable(name, image, monkeypatch):
+    """The batched packs on the side stream (SIDE_STREAM_PACKS): logits bit for bit those of inline
+    packs; an in-place weight update queued on the forward's stream just before the forward is seen
+    (the side stream waits for it); and the forward captures into a HIP graph whose replays match."""
+    torch.manual_seed(5)
+    m = get_model(name, 10, quantizer_dict["po2+"], 4, (image, image)).to(DEV).eval()
+    x = torch.randn(8, 3, image, image, device=DEV)
+    monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", False)
+    with torch.no_grad():
+        m(x)
+        ref = m(x)
+    monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", True)
+    with torch.no_grad():
+        assert torch.equal(m(x), ref)
+        convs = [c for c in m.modules() if isinstance(c, qc.QuantizedConv2d)]
+        for c in convs:
+            c.weight.mul_(0.5)
+        y = m(x)
+        monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", False)
+        ref2 = m(x)
+        monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", True)
+        assert torch.equal(y, ref2)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(x)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = m(x)
+        for _ in range(2):
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref2)
