@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -103,8 +104,8 @@ struct ChainArgs {
 };
 
 // Diagnostic build (-DPO2Q_CHAIN_STAMPS, `make chainstamps`): s_memtime phase stamps, never in the
-// product build.  Phases: 0 prologue (x split), 1 MFMA, 2 barrier after the MFMAs, 3 epilogue,
-// 4 barrier after the epilogue.
+// product build.  Phases per layer: 0 loop top, 1 MFMA, 2 barrier after the MFMAs, 3 epilogue,
+// 4 barrier after the epilogue; once: 5 x loads + split, 6 residual loads, 7 the prologue's barrier.
 #ifdef PO2Q_CHAIN_STAMPS
 #define CHS(i)                                                                           \
     do {                                                                                 \
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     constexpr int WPT = (kChainThreads / 64) / NT;  // waves per output tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 #ifdef PO2Q_CHAIN_STAMPS
-    unsigned ph_[5] = {};
+    unsigned ph_[8] = {};
     unsigned long long tprev_;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev_)::"memory");
 #endif
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             *reinterpret_cast<uint4*>(lds + 2 * a.PL + dst[i]) = lo;
         }
     }
+    CHS(5);
     if (tid < 3) *reinterpret_cast<uint4*>(lds + tid * a.PL + a.ZO) = make_uint4(0u, 0u, 0u, 0u);
     if constexpr (DB) {  // the second set's zero halo (and zero slot): the whole set zeroed once
         for (int i = tid; i < 3 * a.PL / 16; i += kChainThreads)
@@ -210,7 +212,29 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
 #pragma unroll
         for (int i = 0; i < 4; ++i) rres[gi][i] = ok ? xn[(int64_t)(c0 + i) * HW + f] : 0.0f;
     }
+    // ---- the layer descriptors (kernel arguments read with scalar loads at the top of every layer):
+    // one batch of scalar loads over every 64-byte line of the arguments and ONE wait, here where the
+    // residual loads are in flight, so the per-layer descriptor reads hit the scalar cache instead of
+    // each paying a cold miss
+    {
+        static_assert(offsetof(ChainArgs, layer) + sizeof(ChainLayer) * kChainMax + 16 <= 22 * 64 + 60,
+                      "the warm-up below covers 22 lines of kernel arguments");
+        const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+        unsigned d;
+#define PO2Q_WL(o) "s_load_dword %0, %1, " #o "\n\t"
+        asm volatile(PO2Q_WL(0x0) PO2Q_WL(0x40) PO2Q_WL(0x80) PO2Q_WL(0xc0) PO2Q_WL(0x100) PO2Q_WL(0x140)
+                     PO2Q_WL(0x180) PO2Q_WL(0x1c0) PO2Q_WL(0x200) PO2Q_WL(0x240) PO2Q_WL(0x280) PO2Q_WL(0x2c0)
+                     PO2Q_WL(0x300) PO2Q_WL(0x340) PO2Q_WL(0x380) PO2Q_WL(0x3c0) PO2Q_WL(0x400) PO2Q_WL(0x440)
+                     PO2Q_WL(0x480) PO2Q_WL(0x4c0) PO2Q_WL(0x500) PO2Q_WL(0x540) "s_waitcnt lgkmcnt(0)"
+                     : "=&s"(d)
+                     : "s"(kp)
+                     : "memory");
+#undef PO2Q_WL
+        (void)d;
+    }
+    CHS(6);
     __syncthreads();
+    CHS(7);
 
     // this wave's groups: padded pixel of tap (0, 0) per group (past the image: pixel 0, the
     // result is not stored -- every group runs the same unrolled MFMA sequence)
@@ -336,12 +360,19 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         const int rd = DB ? (l & 1) * 3 * a.PL : 0, wr = DB ? ((l + 1) & 1) * 3 * a.PL : 0;
         // this layer's epilogue constants: loaded now, consumed after the MFMA phase
         const float scale = *ly.scale;
-        float cbk[4], ceps[4], cepb[4];
+        // one uniform branch per vector (a per-element test had put 12 scalar branches in the loop top)
+        float cbk[4] = {0.f, 0.f, 0.f, 0.f}, ceps[4] = {1.f, 1.f, 1.f, 1.f}, cepb[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ly.bias) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            cbk[i] = ly.bias ? ly.bias[c0 + i] : 0.0f;
-            ceps[i] = ly.ps ? ly.ps[c0 + i] : 1.0f;
-            cepb[i] = ly.pb ? ly.pb[c0 + i] : 0.0f;
+            for (int i = 0; i < 4; ++i) cbk[i] = ly.bias[c0 + i];
+        }
+        if (ly.ps) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ceps[i] = ly.ps[c0 + i];
+        }
+        if (ly.pb) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cepb[i] = ly.pb[c0 + i];
         }
         // opaque per layer: keeps the step addresses from being hoisted out of the layer loop
         // (one VGPR per step held across every layer)
@@ -463,7 +494,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     }
 #ifdef PO2Q_CHAIN_STAMPS
     if (lane == 0 && a.stamps)
-        for (int i = 0; i < 5; ++i) a.stamps[((size_t)blockIdx.x * 8 + wave) * 5 + i] = ph_[i];
+        for (int i = 0; i < 8; ++i) a.stamps[((size_t)blockIdx.x * 8 + wave) * 8 + i] = ph_[i];
 #endif
 }
 
@@ -682,7 +713,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     }
 #ifdef PO2Q_CHAIN_STAMPS
     if (getenv("PO2Q_STAMPS") && !a.stamps) {  // once more with the stamp buffer, summed per phase
-        const size_t nst = (size_t)N * 8 * 5;
+        const size_t nst = (size_t)N * 8 * 8;
         if (hipMalloc(&a.stamps, nst * 4) == hipSuccess) {
             (void)hipMemsetAsync(a.stamps, 0, nst * 4, s);
             launch(a);
@@ -690,15 +721,18 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
             (void)hipStreamSynchronize(s);
             (void)hipMemcpy(h.data(), a.stamps, nst * 4, hipMemcpyDeviceToHost);
             (void)hipFree(a.stamps);
-            double ph[5] = {0, 0, 0, 0, 0};
+            double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             for (int64_t b = 0; b < N; ++b)
                 for (int w = 0; w < 8; ++w)
-                    for (int i = 0; i < 5; ++i) ph[i] += h[((size_t)b * 8 + w) * 5 + i];
+                    for (int i = 0; i < 8; ++i) ph[i] += h[((size_t)b * 8 + w) * 8 + i];
             fprintf(stderr, "[po2q chain stamps] C=%lld H=%lld W=%lld L=%d db=%d: cycles per layer per wave:", (long long)C,
                     (long long)H, (long long)W, n_layers, db ? 1 : 0);
-            const char* names[5] = {"prologue", "mfma", "bar1", "epilogue", "bar2"};
-            for (int i = 0; i < 5; ++i)
-                fprintf(stderr, " %s %.0f", names[i], ph[i] / (double)(N * 8) / (i ? n_layers : 1));
+            // per layer: top (loop top to the MFMAs: descriptor, epilogue constants; layer 0's also
+            // the groups' address setup), mfma, bar1, epilogue, bar2; once: the prologue's x loads +
+            // split (pro-split), residual loads (pro-res) and block barrier (pro-bar)
+            const char* names[8] = {"top", "mfma", "bar1", "epilogue", "bar2", "pro-split", "pro-res", "pro-bar"};
+            for (int i = 0; i < 8; ++i)
+                fprintf(stderr, " %s %.0f", names[i], ph[i] / (double)(N * 8) / (i <= 4 ? n_layers : 1));
             fprintf(stderr, "\n");
         }
     }

@@ -1,7 +1,7 @@
 """Phase stamps of the small-image chain kernel (diagnostic build lib_chainstamps, `make -C
 po2_quantization_amd/csrc chainstamps`): s_memtime cycle sums per phase (prologue, MFMA, barrier,
 epilogue, barrier) averaged per layer and wave, printed by the library to stderr, for config 2's
-three stage runs (bs 256, BasicBlock form).  ctypes on the C ABI of lib_chainstamps; torch only for
+three stage runs (bs 256, BasicBlock form, then the plain form: no residual held).  ctypes on the C ABI of lib_chainstamps; torch only for
 device buffers.  GPU only."""
 import ctypes
 import os
@@ -21,7 +21,9 @@ def main():
     os.environ["PO2Q_STAMPS"] = "1"
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    for C, H, n in ((16, 32, 17), (32, 16, 17), (64, 8, 17)):
+    import sys
+    for form, C, H, n in [(f, C, H, n) for f in ("basic", "plain") for C, H, n in ((16, 32, 17), (32, 16, 17), (64, 8, 17))]:
+        print("[chain_stamps] form %s C=%d" % (form, C), file=sys.stderr, flush=True)
         N = 256
         x = torch.relu(torch.randn(N, C, H, H, device=dev))
         ws = [torch.randn(C, C, 3, 3, device=dev) * (1.0 / (9 * C) ** 0.5) for _ in range(n)]
@@ -29,7 +31,7 @@ def main():
         pb = [torch.randn(C, device=dev) * 0.1 for _ in range(n)]
         arr = lambda ts: (P * n)(*[t.data_ptr() for t in ts])
         acts = (i32 * n)(*([1] * n))
-        res = (i32 * n)(*[-1 if l % 2 == 0 else l - 1 for l in range(n)])
+        res = (i32 * n)(*[-1 if l % 2 == 0 or form == "plain" else l - 1 for l in range(n)])
         y = torch.empty_like(x)
         nb = L.po2q_qconv2d_chain_workspace_bytes(N, C, H, H, n)
         wsp = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)
