@@ -293,6 +293,7 @@ static bool plan_heuristic(ConvPlan& p, int mode, int bits, int fsr, int flags, 
         std::vector<PlanCand> f32;
         f32s_candidates(p, f32);
         if (!f32.empty()) {
+            std::stable_sort(f32.begin(), f32.end(), [](const PlanCand& u, const PlanCand& v) { return u.cost < v.cost; });
             PlanCand fb{1e30, p};
             const bool fb_ok = plan_fallback(fb.plan);
             if (fb_ok) f32.push_back(fb);
@@ -383,7 +384,7 @@ bool plan_candidates(std::vector<ConvPlan>& out, int64_t N, int64_t C, int64_t H
             const ConvPlan& c = v[i].plan;
             bool dup = false;
             for (const ConvPlan& o : out)
-                dup |= o.kind == c.kind && o.NJ == c.NJ && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
+                dup |= o.kind == c.kind && o.NJ == c.NJ && o.MI == c.MI && o.TP == c.TP && o.TQ == c.TQ && o.vrx == c.vrx &&
                        o.dma_waves == c.dma_waves && o.dma_ov == c.dma_ov &&
                        o.dma_nw == c.dma_nw && o.pd == c.pd && o.nts == c.nts && o.PS == c.PS && o.fp == c.fp &&
                        (c.kind != KIND_BF16X3_IMG || o.kblocks == c.kblocks);

@@ -3,7 +3,7 @@
 // conv as mode "none" with the quantized weight), with the eval BatchNorm / activation /
 // residual of the block in the store:
 //
-//  * conv_direct_f32 -- the 3-input-channel stems: ResNet's conv1 3 -> 16 3x3 s1 (reference
+//  * conv_direct_f32 / conv_stem_f32 -- the 3-input-channel stems: ResNet's conv1 3 -> 16 3x3 s1 (reference
 //    models/resnet.py:99-102, 191), MobileNetV2's features[0] 3 -> 32 3x3 s2
 //    (models/mobilenet.py:41-46, 167), MobileViT's conv1 3 -> 16 3x3 s2 (models/mobile_vit.py:
 //    41-48, 456).  27 MACs per output: a direct VALU conv (fp32 fma, weights wave-uniform), one
@@ -146,6 +146,73 @@ __global__ __launch_bounds__(256) void conv_direct_f32(const float* __restrict__
         with_act(a.act, [&](auto A) __attribute__((always_inline)) { body(A); });
 }
 
+// Direct 3x3 conv, pixel per thread (plan field MI = 1): thread = ONE output pixel (n, p, q) x the
+// KG output channels of blockIdx.y, consecutive lanes on consecutive output columns (each input
+// load and each channel's store is one contiguous run across the wave).  The block's KG x C x 9
+// weights are staged in LDS once and read back as wave-wide broadcasts; the input window is 9C
+// loads from clamped addresses with a select (no per-load branch).  Same sums as conv_direct_f32
+// (fp32 fma in (c, r, s) order from 0), so the two agree bit for bit.
+template <int SH, int CMAX, int KG = 8>
+__global__ __launch_bounds__(256) void conv_stem_f32(const float* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, float* __restrict__ y,
+                                                     F32sArgs a, int epi) {
+    __shared__ float wl[KG * CMAX * 9];
+    const int k0 = (int)blockIdx.y * KG;
+    const int C = a.C;
+    for (int i = threadIdx.x; i < KG * CMAX * 9; i += 256) {
+        const int u = i / (CMAX * 9), rem = i - u * (CMAX * 9), c = rem / 9;
+        const int k = k0 + u;
+        wl[i] = (k < a.K && c < C) ? w[((int64_t)k * C + c) * 9 + (rem - 9 * c)] : 0.0f;
+    }
+    __syncthreads();
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.M) return;
+    const int q = (int)(t % a.Q);
+    const int64_t r0 = t / a.Q;
+    const int p = (int)(r0 % a.P), n = (int)(r0 / a.P);
+    const int h0 = p * SH - a.ph, w0 = q * SH - a.pw;
+    float xv[CMAX][9];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                const int h = h0 + r, ww = w0 + s;
+                const bool ok = c < C && h >= 0 && h < a.H && ww >= 0 && ww < a.W;
+                const float v = x[(((int64_t)n * C + (c < C ? c : 0)) * a.H + (ok ? h : 0)) * a.W + (ok ? ww : 0)];
+                xv[c][r * 3 + s] = ok ? v : 0.0f;
+            }
+    auto body = [&](auto ACT_) __attribute__((always_inline)) {
+        constexpr int ACT = decltype(ACT_)::value;
+        constexpr bool E = ACT >= 0;
+#pragma unroll
+        for (int u = 0; u < KG; ++u) {
+            const int k = k0 + u;
+            if (k >= a.K) break;  // block-uniform
+            float acc = 0.0f;
+#pragma unroll
+            for (int c = 0; c < CMAX; ++c) {
+                if (c >= C) break;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) acc = fmaf(xv[c][j], wl[(u * CMAX + c) * 9 + j], acc);
+            }
+            float v = acc + (bias ? bias[k] : 0.0f);
+            const int64_t off = (((int64_t)n * a.K + k) * a.P + p) * a.Q + q;
+            if constexpr (E) {
+                v = v * (a.ps ? a.ps[k] : 1.0f) + (a.pb ? a.pb[k] : 0.0f);
+                if (a.res) v += a.res[off];
+                v = epi_act_ct<E ? ACT : 0>(v);
+            }
+            y[off] = v;
+        }
+    };
+    if (epi == 0)
+        body(std::integral_constant<int, -1>{});
+    else
+        with_act(a.act, [&](auto A) __attribute__((always_inline)) { body(A); });
+}
+
 // Pointwise 1x1 fp32 GEMM on v_mfma_f32_16x16x4_f32: wave = MI groups of 16 pixels x KT tiles of
 // 16 output channels; per MFMA a lane holds one x value (pixel l & 15, channel 4 j + (l >> 4)) and
 // one weight (output channel l & 15 of the tile, same channel): exact products, fp32 sums.  Every
@@ -268,7 +335,16 @@ void f32s_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
             p.MI = kb;
             PlanCand c;
             c.plan = p;
-            c.cost = kb == 16 ? (items >= 65536 ? 0.0 : 1.0) : (items >= 65536 ? 1.0 : 0.0);
+            c.cost = kb == 16 ? (items >= 65536 ? 0.5 : 1.0) : (items >= 65536 ? 1.0 : 0.5);
+            out.push_back(c);
+        }
+        {  // MI 1: conv_stem_f32, one output pixel x 8 channels per thread (the default)
+            ConvPlan q = p;
+            q.MI = 1;
+            q.blocks = ((int64_t)base.N * base.P * base.Q + 255) / 256;
+            PlanCand c;
+            c.plan = q;
+            c.cost = 0.0;
             out.push_back(c);
         }
     }
@@ -304,6 +380,18 @@ hipError_t launch_conv_f32s(const ConvPlan& p, const float* x, const float* w, c
     a.ps = ps; a.pb = pb; a.res = res; a.act = act;
     a.M = (int64_t)p.N * p.P * p.Q;
     const int epi = (ps || pb || res || act != 0) ? 1 : 0;
+    if (p.kind == KIND_DIRECT_F32 && p.MI == 1) {
+        const dim3 grid((unsigned)((a.M + 255) / 256), (unsigned)((p.K + 7) / 8)), block(256);
+        if (p.vrx == 1 && p.NJ == 3)
+            hipLaunchKernelGGL((conv_stem_f32<1, 3>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else if (p.vrx == 1)
+            hipLaunchKernelGGL((conv_stem_f32<1, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else if (p.NJ == 3)
+            hipLaunchKernelGGL((conv_stem_f32<2, 3>), grid, block, 0, s, x, w, bias, y, a, epi);
+        else
+            hipLaunchKernelGGL((conv_stem_f32<2, 4>), grid, block, 0, s, x, w, bias, y, a, epi);
+        return hipGetLastError();
+    }
     if (p.kind == KIND_DIRECT_F32) {
         a.Q4 = (p.Q + 3) / 4;
         a.items = p.N * p.P * a.Q4;
