@@ -856,7 +856,7 @@ def main():
                                    % (" and stage-2" if pair32_used else "")) if pair_used else "",
                                   " (stride-2 conv1 + 1x1 shortcut of stages 2-3 as one launch each)"
                                   if s2ds_used else "",
-                                  " (weight packs of the single-conv layers batched: one launch per 24)"
+                                  " (weight packs of the single-conv layers batched: one launch per 36)"
                                   if chain.packed is not None else "",
                                   " + RCCL all_gather(logits)" if world > 1 else ""),
                    "conv_pairs": pair_used,

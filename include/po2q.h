@@ -346,7 +346,7 @@ void po2q_qconv2d_plan_destroy(po2q_conv_plan* plan);
  * QuantizedConv2d.forward quantizes its weight, models/quantized_conv.py:32-38): for every
  * plans[i] whose kernel does not stage its weight itself, quantize + pack w[i] into
  * workspace[i] (>= po2q_qconv2d_plan_workspace_bytes) -- the bf16x3 packs in
- * ceil(n / 24) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
+ * ceil(n / 36) launches instead of n.  po2q_qconv2d_plan_run_packed then runs plan's conv
  * from that workspace (w is read only by plans that stage their weight in-kernel); on one
  * stream the pair equals po2q_qconv2d_plan_run bit for bit.  The plans may differ in bits /
  * fsr / mode; depthwise plans join the batched launches too (their plain quantized copy).

@@ -659,7 +659,7 @@ class PackedConvs:
     """Several QuantizedConv2d forwards (models/quantized_conv.py:32-38) with their weight
     quantize + pack as ONE batched launch (po2q_qconv2d_plan_pack_batch) and each conv from its
     packed workspace (po2q_qconv2d_plan_run_packed) -- the same kernels and results as
-    qconv2d() layer by layer, with ceil(n / 24) pack launches instead of one per layer.
+    qconv2d() layer by layer, with ceil(n / 36) pack launches instead of one per layer.
 
     specs: [(x_shape, w, stride, padding)] in call order (groups 1, dilation 1, no bias); the
     plans are resolved once here, so create it after the shapes were autotuned.  Call pack()

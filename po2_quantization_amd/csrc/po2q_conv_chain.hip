@@ -624,7 +624,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     char* ws = reinterpret_cast<char*>(workspace);
 
-    // every layer's weight: quantize + pack in ceil(n / 24) launches
+    // every layer's weight: quantize + pack in ceil(n / 36) launches
     const ConvPlan plan = chain_plan(N, C, H, W);
     std::vector<const ConvPlan*> plans((size_t)n_layers, &plan);
     std::vector<uint16_t*> packed((size_t)n_layers);

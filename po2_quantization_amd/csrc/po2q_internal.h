@@ -166,7 +166,7 @@ struct PackReq {
 // whether a plan's weight staging can join a batched pack (quantized, fused absmax size,
 // bf16x3 or depthwise kind)
 bool pack_batchable(const ConvPlan& p, int mode);
-// n weight tensors (pack_batchable plans, each with its own bits / fsr / mode) in ceil(n / 24) launches
+// n weight tensors (pack_batchable plans, each with its own bits / fsr / mode) in ceil(n / 36) launches
 hipError_t launch_pack_batch(int n, const PackReq* reqs, hipStream_t s);
 // The same for n bf16x3 weight tensors with one (bits, fsr, mode).
 hipError_t launch_pack_bf16x3_batch(int n, const ConvPlan* const* plans, const float* const* w,

@@ -307,7 +307,7 @@ struct PackJob {
     int lo, hi, mode, nb, plain, nparts;
     PackX3 pg;
 };
-constexpr int kPackBatch = 24;  // 24 x 104-byte jobs: 2.5 KB of kernel arguments
+constexpr int kPackBatch = 36;  // 36 x 104-byte jobs: 3.7 KB of kernel arguments (the limit is 4 KB)
 struct PackBatch {
     PackJob job[kPackBatch];
 };

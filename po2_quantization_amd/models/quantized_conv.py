@@ -162,7 +162,7 @@ def can_fuse(*mods):
 # its own forward, quantized_conv.py:35).  Layers whose kernel reads a pre-packed weight (the
 # single-conv row / pointwise / depthwise plans; the pair, stride-2, chain and fused-staging
 # kernels quantize their weights themselves) get their quantize + pack from ONE batched launch
-# per 24 layers at the start of the forward (torch.ops.po2q.qconv2d_pack_batch), then run from
+# per 36 layers at the start of the forward (torch.ops.po2q.qconv2d_pack_batch), then run from
 # the packed workspace (qconv2d_packed): the same plans and results, bit for bit, with every
 # weight still re-quantized in every forward.  The first forward of a model at an input shape
 # records which layers do that and at which shapes; later forwards at that shape pack them
