@@ -495,6 +495,32 @@ def test_nonfinite_inputs_pair_and_s2ds(C, W):
     assert _same_nonfinite(yd.cpu(), _oracle_ref(x, wd, 2, 0))
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 10, 112), (3, 30, 112), (1, 17, 112), (2, 112, 112)])
+def test_s2ds_two_segment_blocks_bitwise_equal(N, H, W, monkeypatch):
+    """The C = 32 fused transition with two segments per block (SEG2, PO2Q_S2DS_SEG2=1) against the
+    one-segment kernel (the default): same arithmetic, the same bits, with the eval affine / ReLU
+    epilogue; and the shortcut and conv outputs against the oracle (odd segment counts leave an empty
+    half)."""
+    C = 32
+    g = torch.Generator().manual_seed(N * 7 + H + W)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    w3 = (torch.randn(2 * C, C, 3, 3, generator=g) * 0.1).to(DEV)
+    wd = (torch.randn(2 * C, C, 1, 1, generator=g) * 0.2).to(DEV)
+    ps, pb = (torch.rand(2 * C, generator=g) + 0.5).to(DEV), (torch.randn(2 * C, generator=g) * 0.1).to(DEV)
+    monkeypatch.setenv("PO2Q_S2DS_SEG2", "0")
+    r3, rd = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2")
+    e3, ed = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2", post_scale=ps, post_shift=pb, act="relu")
+    monkeypatch.setenv("PO2Q_S2DS_SEG2", "1")
+    y3, yd = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2")
+    f3, fd = _lib.qconv2d_s2ds(x, w3, wd, 4, "po2", post_scale=ps, post_shift=pb, act="relu")
+    assert torch.equal(y3, r3) and torch.equal(yd, rd)
+    assert torch.equal(f3, e3) and torch.equal(fd, ed)
+    ref3, _ = O.qconv2d(x.cpu().numpy(), w3.cpu().numpy(), None, 2, 1, 1, 1, 4, "po2")
+    refd, _ = O.qconv2d(x.cpu().numpy(), wd.cpu().numpy(), None, 2, 0, 1, 1, 4, "po2")
+    assert normwise_err(y3.cpu().numpy(), ref3) <= CONV_TOL
+    assert normwise_err(yd.cpu().numpy(), refd) <= CONV_TOL
+
+
 PW_SHAPES = [  # N, C, HW side, K: MobileNetV2 @32 expand / project convs and odd edges
     (4, 16, 16, 96), (4, 96, 8, 24), (3, 24, 8, 144), (4, 144, 4, 32), (5, 160, 2, 960), (5, 960, 2, 160),
     (3, 32, 7, 64),   # HW = 49: 16-pixel groups span images, scalar stores
