@@ -140,6 +140,19 @@ def test_plan_enumeration_on_host():
     assert b"out of range" in L.po2q_last_error()
 
 
+def test_fp32_plan_variants_on_host():
+    """Unquantized stems and 1x1 convs: the pixel-per-thread stem kernel (MI 1) is the default and the
+    4- / 16-channel direct variants follow it; the fp32 pointwise GEMM offers its 2- and 4-group
+    variants.  Candidates that differ only in MI are distinct (the plan list keys on MI)."""
+    stem = _lib.plans(256, 3, 32, 32, 32, 3, 3, 2, 1, mode="none")
+    direct = [p for p in stem if "kind=direct_f32" in p]
+    assert [p.split(" MI=")[1].split()[0] for p in direct] == ["1", "4", "16"], direct
+    assert stem[0] == _lib.describe(256, 3, 32, 32, 32, 3, 3, 2, 1, mode="none") == direct[0]
+    pw = [p for p in _lib.plans(256, 320, 4, 4, 1280, 1, 1, 1, 0, mode="none") if "kind=pw_f32" in p]
+    assert {p.split(" MI=")[1].split()[0] for p in pw} == {"1", "2", "4"}, pw
+    assert len(set(stem)) == len(stem)
+
+
 def test_small_image_plans_on_host():
     """CIFAR-size 3x3 / stride-1 convs (ResNet56 @32: 32x32 x 16, 16x16 x 32, 8x8 x 64) default to
     the LDS-resident small-image kernel and offer its row-segment / channel-group variants to the
