@@ -356,7 +356,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     };
 
     for (int l = 0; l < a.L; ++l) {
-        const ChainLayer& ly = a.layer[l];
+        const ChainLayer ly = a.layer[l];  // one batch of scalar loads for the whole descriptor
         const int rd = DB ? (l & 1) * 3 * a.PL : 0, wr = DB ? ((l + 1) & 1) * 3 * a.PL : 0;
         // this layer's epilogue constants: loaded now, consumed after the MFMA phase
         const float scale = *ly.scale;
