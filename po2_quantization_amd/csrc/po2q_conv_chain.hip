@@ -99,6 +99,7 @@ struct ChainArgs {
     int H, W, L;
     int PW, PL, ZO;
     int res0;             // 1: x itself is a later layer's residual: hold it
+    int prio;             // 1: the second wave of each SIMD (waves 4..7) issues at priority 1
     unsigned* stamps;     // PO2Q_CHAIN_STAMPS diagnostic builds only: per (block, wave) phase cycle sums
     ChainLayer layer[kChainMax];
 };
@@ -355,6 +356,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         static_for<S1>(step);
     };
 
+    if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
     for (int l = 0; l < a.L; ++l) {
         const ChainLayer ly = a.layer[l];  // one batch of scalar loads for the whole descriptor
         const int rd = DB ? (l & 1) * 3 * a.PL : 0, wr = DB ? ((l + 1) & 1) * 3 * a.PL : 0;
@@ -650,6 +652,11 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     a.PL = (int)chain_plane(C, H, W);
     a.ZO = a.PL - 16;
     a.res0 = used[0];
+    {  // PO2Q_CHAIN_PRIO=1: waves 4..7 at issue priority 1 (A/B knob; off: config 2 827.5k vs 826.7k
+       // img/s, 4 interleaved rounds, profiles/r05_ab_chain_prio.jsonl)
+        const char* pe = getenv("PO2Q_CHAIN_PRIO");
+        a.prio = (pe && pe[0] == '1') ? 1 : 0;
+    }
     for (int l = 0; l < n_layers; ++l) {
         ChainLayer& ly = a.layer[l];
         ly.wp = reinterpret_cast<const uint4*>(packed[l]);
