@@ -1,34 +1,25 @@
-"""Run the small-image chain kernel (po2q_qconv2d_chain_f32) a few times for rocprofv3 kernel
-traces / PMC counters: config 2's stage runs (ResNet56 @32, bs = 256).
-
-    python tools/prof_chain.py --stage 1 --iters 5
-"""
-import argparse
+"""Driver for PMC passes over the small-image chain kernel (tools/pmc.sh via PMC_DRIVER, or rocprofv3
+directly): config 2's stage-1 run (bs 256, 16 x 32 x 32, 17 layers, BasicBlock form) launched a few
+times.  GPU only, tuning aid."""
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from po2_quantization_amd import _lib  # noqa: E402
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--stage", type=int, default=1, help="1: 18 x 16->16 @32, 2: 17 x 32->32 @16, 3: 17 x 64->64 @8")
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--iters", type=int, default=5)
-    args = ap.parse_args()
-    from po2_quantization_amd import _lib
-
-    C, H, n = {1: (16, 32, 18), 2: (32, 16, 17), 3: (64, 8, 17)}[args.stage]
+    C, H, n = int(os.environ.get("CHAIN_C", 16)), int(os.environ.get("CHAIN_H", 32)), 17
     dev = torch.device("cuda:0")
-    torch.manual_seed(0)
-    x = torch.relu(torch.randn(args.batch, C, H, H, device=dev))
-    ws = [torch.randn(C, C, 3, 3, device=dev) * 0.1 for _ in range(n)]
-    print("PLAN chain stage %d: %d x %d->%d @%dx%d bs=%d" % (args.stage, n, C, C, H, H, args.batch), flush=True)
-    for _ in range(args.iters):
-        _lib.qconv2d_chain(x, ws, 4, "po2")
+    x = torch.relu(torch.randn(256, C, H, H, device=dev))
+    ws = [torch.randn(C, C, 3, 3, device=dev) * (1.0 / (9 * C) ** 0.5) for _ in range(n)]
+    ps = [torch.rand(C, device=dev) + 0.5 for _ in range(n)]
+    pb = [torch.randn(C, device=dev) * 0.1 for _ in range(n)]
+    res = [-1 if l % 2 == 0 else l - 1 for l in range(n)]
+    for _ in range(3):
+        _lib.qconv2d_chain(x, ws, 4, "po2", post_scales=ps, post_shifts=pb, acts=["relu"] * n, res_from=res)
     torch.cuda.synchronize()
 
 
