@@ -56,12 +56,16 @@ constexpr size_t kChainLdsMax = 160 * 1024;
 // group is two 8-pixel row pieces 10 padded pixels apart): the octet XORed with a per-column
 // table instead (exhaustive search over every tap offset, tools-free: 3 bits per column).
 template <int C, bool W8 = false, bool S16 = false>
-__device__ __forceinline__ int ch_addr(int pp, int col, int oc) {
+__device__ __forceinline__ int ch_addr(int pp, int col, int oc, int oct = 0) {
     if constexpr (C == 16) {
-        // S16 (A/B only): the octet flipped with pixel bit 2 -- by the bank model conflict-free
-        // for the reads and half the epilogue ds_write_b64 conflicts, yet 11 % slower measured
-        // (profiles/r03_chain_ab.json), so the product layout stays unswizzled
-        return pp * 32 + 16 * (S16 ? (oc ^ ((pp >> 2) & 1)) : oc);
+        // S16 (PO2Q_CHAIN_VARIANT bit 1): octet-major planes, [octet][pixel][8 ch] (oct = bytes per
+        // octet half-plane): 16 consecutive pixels of one octet are 256 contiguous bytes, so the
+        // fragment reads (ds_read_b128) and the epilogue writes (ds_write_b64) of a 16-lane group hit
+        // distinct banks; [pixel][octet] (the default) puts pixels p and p + 8 on the same banks
+        // (PMC: 34 % of the LDS cycles conflicted, profiles/r05_pmc_chain16.json).  Measured slower all
+        // the same: the MFMA phase 4,570 -> 6,316 cycles per layer, config 2 827k -> 776k img/s
+        // (profiles/r05_ab_chain_octet_major.jsonl, r05_chain_stamps_octet_major.txt), so it stays off
+        return S16 ? oc * oct + pp * 16 : pp * 32 + 16 * oc;
     } else if constexpr (C == 32) {
         return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
     } else if constexpr (W8) {
@@ -163,6 +167,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     const int n = blockIdx.x;
     const int nt = wave % NT, gsub = wave / NT;
     const int H = a.H, W = a.W, PW = a.PW, HW = H * W;
+    const int OCT = (H + 2) * PW * 16;  // S16 (C = 16): bytes per octet half-plane
     const int ngroups = (HW + 15) >> 4;
     const int p = lane & 15, g4 = lane >> 4;
     const int c0 = 16 * nt + 4 * g4;  // this lane's 4 output channels (transposed form)
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
-            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc) : -1;
+            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc, OCT) : -1;
         }
 #pragma unroll
         for (int i = 0; i < kChainItems; ++i) {
@@ -255,7 +260,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         constexpr int gi = st / (3 * KS), t = st % (3 * KS), r = t / KS, ks = t % KS;
         if constexpr (C == 16) {
             const int s = ks == 0 ? (g4 >> 1) : 2;
-            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1);
+            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1, OCT);
         } else {
             return ch_addr<C, W8, S16>(pp0[gi] + r * PW + ks % 3, px0[gi] + ks % 3, (ks / 3) * 4 + g4);
         }
@@ -307,33 +312,25 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         // (s0 | s1) steps, or plus a per-lane offset (the two k-halves' tap rows / planes) for the
         // paired s2 steps.  The last pair's zero half reads the r2 lo unit again (finite: the split
         // clamps mid / lo) against zero weights, so it needs no zero slot.
+        // pixel pitch and octet offset: [pixel][octet] (32 B, 16 B) or, S16, [octet][pixel] (16 B, OCT)
+        constexpr int PXB = S16 ? 16 : 32;
+        const int OCB = S16 ? OCT : 16;
         int lb[MG], dsel[5];
 #pragma unroll
-        for (int gi = 0; gi < MG; ++gi) lb[gi] = (pp0[gi] + 2) * 32 + 16 * (g4 & 1);  // tap s = 2
+        for (int gi = 0; gi < MG; ++gi) lb[gi] = (pp0[gi] + 2) * PXB + OCB * (g4 & 1);  // tap s = 2
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
             const int ua = 2 * u, ub = u == 4 ? 8 : 2 * u + 1;
             const int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
-            dsel[u] = g4 < 2 ? ra * PW * 32 + pa * a.PL : rb * PW * 32 + pb * a.PL;
+            dsel[u] = g4 < 2 ? ra * PW * PXB + pa * a.PL : rb * PW * PXB + pb * a.PL;
         }
-        const int s01 = ((g4 >> 1) - 2) * 32;  // tap (g4 >> 1) relative to the s = 2 base
+        const int s01 = ((g4 >> 1) - 2) * PXB;  // tap (g4 >> 1) relative to the s = 2 base
         auto addr = [&](auto ST_) __attribute__((always_inline)) {
             constexpr int st = decltype(ST_)::value;
             constexpr int t = FULL ? st / MG : st % T1, gi = FULL ? st % MG : st / T1;  // FULL: k-step major
-            if constexpr (S16) {  // A/B layout: the generic address
-                if constexpr (t < 9) {
-                    constexpr int r = t / 3, pl = t % 3;
-                    const int s = g4 >> 1;
-                    return pl * a.PL + ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1);
-                } else {
-                    constexpr int ua = 2 * (t - 9), ub = t == 13 ? 8 : ua + 1;
-                    constexpr int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
-                    if (g4 < 2) return pa * a.PL + ch_addr<C, W8, S16>(pp0[gi] + ra * PW + 2, px0[gi] + 2, g4 & 1);
-                    return pb * a.PL + ch_addr<C, W8, S16>(pp0[gi] + rb * PW + 2, px0[gi] + 2, g4 & 1);
-                }
-            } else if constexpr (t < 9) {
+            if constexpr (t < 9) {
                 constexpr int r = t / 3, pl = t % 3;
-                return lb[gi] + s01 + (r * PW * 32 + pl * a.PL);
+                return lb[gi] + s01 + (r * PW * PXB + pl * a.PL);
             } else {
                 return lb[gi] + dsel[t - 9];
             }
@@ -471,7 +468,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 } else {
                     // padded pixel (oy + 1, ox + 1) of output pixel f = (oy, ox): pp0 / px0 hold (oy, ox) of
                     // tap (0, 0), so no division by W here
-                    const int ad = ch_addr<C, W8, S16>(pp0[gi] + PW + 1, px0[gi] + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
+                    const int ad = ch_addr<C, W8, S16>(pp0[gi] + PW + 1, px0[gi] + 1, c0 >> 3, OCT) + 8 * ((c0 >> 2) & 1);
                     uint2 hi, mid, lo;
                     const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                                             __float_as_uint(v[3])};
