@@ -58,14 +58,16 @@ constexpr size_t kChainLdsMax = 160 * 1024;
 template <int C, bool W8 = false, bool S16 = false>
 __device__ __forceinline__ int ch_addr(int pp, int col, int oc, int oct = 0) {
     if constexpr (C == 16) {
-        // S16 (PO2Q_CHAIN_VARIANT bit 1): octet-major planes, [octet][pixel][8 ch] (oct = bytes per
-        // octet half-plane): 16 consecutive pixels of one octet are 256 contiguous bytes, so the
-        // fragment reads (ds_read_b128) and the epilogue writes (ds_write_b64) of a 16-lane group hit
-        // distinct banks; [pixel][octet] (the default) puts pixels p and p + 8 on the same banks
-        // (PMC: 34 % of the LDS cycles conflicted, profiles/r05_pmc_chain16.json).  Measured slower all
-        // the same: the MFMA phase 4,570 -> 6,316 cycles per layer, config 2 827k -> 776k img/s
-        // (profiles/r05_ab_chain_octet_major.jsonl, r05_chain_stamps_octet_major.txt), so it stays off
-        return S16 ? oc * oct + pp * 16 : pp * 32 + 16 * oc;
+        // S16 (PO2Q_CHAIN_VARIANT bit 1): the octet flipped with pixel bit 3, so pixels p and p + 8 of a
+        // 16-pixel group sit on different banks for the fragment reads (ds_read_b128) and the epilogue
+        // writes (ds_write_b64); [pixel][octet] (the default) puts them on the same banks (PMC: 34 % of
+        // the LDS cycles conflicted, profiles/r05_pmc_chain16.json; tools/lds_probe.hip: reads 81 vs 49
+        // cycles, writes 112 vs 61).  Measured slower in the kernel all the same, like the octet-major
+        // layout tried first ([octet][pixel]): MFMA phase 4,570 -> 7,258 cycles per layer, epilogue
+        // unchanged, config 2 813k -> 759k img/s (r05_ab_chain_bit3.jsonl, r05_chain_stamps_bit3.txt;
+        // octet-major: r05_ab_chain_octet_major.jsonl) -- the conflicts are not what bounds the chain,
+        // the per-step address work (pinned by the sched_barriers) is.  Off.  oct: unused
+        return S16 ? pp * 32 + 16 * (oc ^ ((pp >> 3) & 1)) : pp * 32 + 16 * oc;
     } else if constexpr (C == 32) {
         return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
     } else if constexpr (W8) {
@@ -312,10 +314,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         // (s0 | s1) steps, or plus a per-lane offset (the two k-halves' tap rows / planes) for the
         // paired s2 steps.  The last pair's zero half reads the r2 lo unit again (finite: the split
         // clamps mid / lo) against zero weights, so it needs no zero slot.
-        // pixel pitch and octet offset: [pixel][octet] (32 B, 16 B) or, S16, [octet][pixel] (16 B, OCT)
-        constexpr int PXB = S16 ? 16 : 32;
-        const int OCB = S16 ? OCT : 16;
-        int lb[MG], dsel[5];
+        // S16: the swizzle flips address bit 4 (the octet) with bit 8 (pixel bit 3) of the pixel's
+        // address within its plane; the plane offset is added after the flip
+        constexpr int PXB = 32;
+        const int OCB = 16;
+        (void)OCT;
+        int lb[MG], dsel[5], drow[5], dpl[5];
 #pragma unroll
         for (int gi = 0; gi < MG; ++gi) lb[gi] = (pp0[gi] + 2) * PXB + OCB * (g4 & 1);  // tap s = 2
 #pragma unroll
@@ -323,12 +327,22 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             const int ua = 2 * u, ub = u == 4 ? 8 : 2 * u + 1;
             const int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
             dsel[u] = g4 < 2 ? ra * PW * PXB + pa * a.PL : rb * PW * PXB + pb * a.PL;
+            drow[u] = g4 < 2 ? ra * PW * PXB : rb * PW * PXB;
+            dpl[u] = g4 < 2 ? pa * a.PL : pb * a.PL;
         }
         const int s01 = ((g4 >> 1) - 2) * PXB;  // tap (g4 >> 1) relative to the s = 2 base
+        auto flip = [](int b) __attribute__((always_inline)) { return b ^ ((b >> 4) & 16); };
         auto addr = [&](auto ST_) __attribute__((always_inline)) {
             constexpr int st = decltype(ST_)::value;
             constexpr int t = FULL ? st / MG : st % T1, gi = FULL ? st % MG : st / T1;  // FULL: k-step major
-            if constexpr (t < 9) {
+            if constexpr (S16) {
+                if constexpr (t < 9) {
+                    constexpr int r = t / 3, pl = t % 3;
+                    return flip(lb[gi] + s01 + r * PW * PXB) + pl * a.PL;
+                } else {
+                    return flip(lb[gi] + drow[t - 9]) + dpl[t - 9];
+                }
+            } else if constexpr (t < 9) {
                 constexpr int r = t / 3, pl = t % 3;
                 return lb[gi] + s01 + (r * PW * PXB + pl * a.PL);
             } else {
