@@ -260,9 +260,35 @@ def quantize(w, bits, mode, fsr=1):
     return out
 
 
+def restated_quantize_lin(w, bits, plus, num_iters=10):
+    """lin / lin+ for CPU tensors: the reference's per-input-channel refit (utils/quantizers.py:8-16,
+    59-136) as the same torch ops in the same order, so on CPU it is the reference's own arithmetic.
+    The channel axis is dim 1; its step broadcasts over (C, R, S) as the reference's view(-1, 1, 1)."""
+    if w.dim() != 4:
+        raise Po2qError("po2q: the lin quantizers need a 4-D weight (got %d dims)" % w.dim())
+    top = 2 ** (bits - 1) - 1
+
+    def snap(step):  # quantize_per_filter(w, step, bits) / step
+        s = step.view(-1, 1, 1)
+        return (s * torch.clamp(torch.round(w / s), min=-top, max=top)) / s
+
+    hi = w.max(dim=3).values.max(dim=2).values.max(dim=0).values
+    lo = w.min(dim=3).values.min(dim=2).values.min(dim=0).values
+    step = (hi - lo) / (2 ** bits - 1)
+    q = snap(step)
+    shrink = torch.sqrt(torch.tensor(8.0 / 9.0)) if plus else None
+    for _ in range(num_iters):
+        step = torch.sum(q * w, dim=[0, 2, 3]) / torch.sum(q * q, dim=[0, 2, 3])
+        step = 2 ** torch.round(torch.log2(shrink * step if plus else step))
+        q = snap(step)
+    return q * step.view(-1, 1, 1)
+
+
 def quantize_lin(w, bits, plus, num_iters=10):
     """lin / lin+ quantization of a 4-D weight, per input channel (dim 1)
-    (utils/quantizers.py:59-136)."""
+    (utils/quantizers.py:59-136).  CPU tensors take restated_quantize_lin."""
+    if isinstance(w, torch.Tensor) and not w.is_cuda:
+        return restated_quantize_lin(w, int(bits), plus, int(num_iters))
     _require_hip_f32(w, "input")
     if w.dim() != 4:
         # the reference reduces dims 3, 2, 0 explicitly (torch.max(..., dim=3) ...)

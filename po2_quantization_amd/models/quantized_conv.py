@@ -15,7 +15,9 @@ Backward (QAT) keeps the reference's semantics: straight-through estimator on
 the weight (quantizers.py:34-36), conv gradients of the quantized weight -- the input
 gradient through the native conv kernels (strided layers on zero-inserted dy), the weight
 gradient through the native fp32 wgrad kernels, dense and depthwise (_QConv2dFn.backward).
-Inputs must be fp32 HIP tensors; there is no CPU path.
+HIP inputs must be fp32 (anything else raises; there is no silent fallback on the GPU).  CPU
+inputs take the reference's own torch arithmetic (`_torch_forward`: the product's restated
+quantizers + F.conv2d, never the oracle, never libpo2q), as the reference runs on any device.
 
 Inference fusion: `fused(x, bn=, act=, residual=)` runs the conv
 together with the eval BatchNorm that follows it in the reference's blocks (folded
@@ -104,6 +106,17 @@ class _QConv2dFn(torch.autograd.Function):
 
 
 _ACT_NAMES = {nn.ReLU: "relu", nn.ReLU6: "relu6", nn.SiLU: "silu"}
+_ACT_FNS = {"relu": torch.relu, "relu6": nn.functional.relu6, "silu": nn.functional.silu}
+
+
+def _torch_epilogue(y, bn, act, residual):
+    """bn(y) (+ residual), then the activation: the reference blocks' module order (resnet.py:64-67,
+    mobilenet.py:133-134, mobile_vit.py:229-230), for the CPU path of the fused calls."""
+    if bn is not None:
+        y = bn(y)
+    if residual is not None:
+        y = y + residual
+    return _ACT_FNS[act](y) if act else y
 
 
 def act_name(m):
@@ -317,8 +330,19 @@ class QuantizedConv2d(nn.Conv2d):
                              self.bits, mode, self.precision)
         return y.squeeze(0) if unbatched else y
 
+    def _torch_forward(self, input):
+        """The reference's forward as torch ops (quantized_conv.py:32-38): F.conv2d of the quantized
+        weight.  Taken for CPU tensors only -- the HIP kernels never see them -- with the product's
+        own quantizers (PO2 / PO2+ via _lib.restated_quantize, lin / lin+ via
+        _lib.restated_quantize_lin: the reference's torch arithmetic, bit for bit on CPU)."""
+        if self.quantize_fn is None:
+            return self._conv_forward(input, self.weight, self.bias)
+        return self._conv_forward(input, self.quantize_fn.apply(self.weight, self.bits), self.bias)
+
     def forward(self, input):
         # reference quantized_conv.py:32-38
+        if not input.is_cuda:
+            return self._torch_forward(input)
         if self.quantize_fn is None:
             return self._native(input, self.weight, "none")
         mode = NATIVE_MODES.get(self.quantize_fn)
@@ -331,6 +355,8 @@ class QuantizedConv2d(nn.Conv2d):
         """act(bn(self(input)) + residual) in one native call (eval, no autograd; see
         can_fuse).  bn: the following eval BatchNorm or None; act: None | 'relu' |
         'relu6' | 'silu'."""
+        if not input.is_cuda:  # CPU: the reference's module sequence (conv -> bn -> + residual -> act)
+            return _torch_epilogue(self(input), bn, act, residual)
         if self.padding_mode != "zeros":
             raise RuntimeError("po2q: only padding_mode='zeros' is supported (the reference uses the default)")
         mode = "none" if self.quantize_fn is None else NATIVE_MODES.get(self.quantize_fn)
@@ -380,6 +406,8 @@ def plain_conv_fused(conv, x, bn=None, act=None, residual=None):
     """An unquantized nn.Conv2d (the reference's stems and last 1x1 convs: resnet.py:99-102,
     mobilenet.py:41-50, mobile_vit.py:41-48) with the eval BatchNorm / activation after it, as
     ONE native call of the fp32 path (mode "none": exact fp32 products, fp32 accumulation)."""
+    if not x.is_cuda:
+        return _torch_epilogue(conv(x), bn, act, residual)
     if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         raise RuntimeError("po2q: fused plain conv needs numeric zero padding")
     ps, pb = fold_bn(bn) if bn is not None else (None, None)

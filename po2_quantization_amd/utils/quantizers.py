@@ -11,12 +11,13 @@ PO2 / PO2+ on fp32 HIP tensors run on the hand-written HIP kernels of libpo2q.
 The reference's quantizers take any tensor (they are plain torch ops), so CPU,
 fp64 and bf16 inputs go to _lib.restated_quantize, the product-side torch
 restatement of the same threshold-table decision (bit-exact with the reference
-on tests/golden/quant_kat_dtypes.npz); the conv itself has no CPU path.  Backward is the
-straight-through estimator of the reference (:34-36, :54-56).
+on tests/golden/quant_kat_dtypes.npz).  Backward is the straight-through estimator of the
+reference (:34-36, :54-56).
 
 LinearPowerOfTwo(Plus)Quantizer (utils/quantizers.py:59-136)
-run on the native per-channel kernel po2q_quantize_lin_f32 (po2q_lin.hip):
-fp32 HIP 4-D weights only, like the PO2 classes.
+run on the native per-channel kernel po2q_quantize_lin_f32 (po2q_lin.hip) for fp32
+HIP 4-D weights, and on _lib.restated_quantize_lin (the reference's torch ops) for
+CPU tensors.
 """
 from typing import Callable, Optional
 
