@@ -271,13 +271,35 @@ def cpu_baseline(layers, weights_cpu, image, mode, bits, seconds, nb=2):
                       "+ torch CPU F.conv2d/oneDNN, %d threads), %.1f s" % (reps, nb, image, image, threads, dt)}
 
 
-def gather_logits(logits, gathered, world):
+def gather_logits(logits, gathered, world=None):
     """Output gather of the batch-sharded inference: rank r's logits land in rows
-    [r*B, (r+1)*B) of `gathered` on every rank (RCCL all_gather over xGMI)."""
-    if world > 1:
+    [r*B, (r+1)*B) of `gathered` on every rank (RCCL all_gather over xGMI).  The collective runs
+    whenever a process group exists and `gathered` was allocated for it (gather_buffer), a
+    one-rank group included; without a group the logits are the output."""
+    if gathered is not None:
         dist.all_gather_into_tensor(gathered, logits.contiguous())
         return gathered
     return logits
+
+
+def gather_buffer(rows, classes, dev):
+    """The all_gather target of gather_logits: [world * rows, classes] when a process group exists."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return torch.empty(dist.get_world_size() * rows, classes, device=dev)
+
+
+def leg_steps(replay, floor, seconds, probe=20):
+    """Timed steps of a graph-replayed config leg: at least `floor`, and enough for `seconds` of GPU work
+    (estimated from `probe` untimed replays), so an outside sampler of GPU activity sees the leg."""
+    replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(probe):
+        replay()
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t0) / probe
+    return max(int(floor), int(math.ceil(seconds / max(per, 1e-6))))
 
 
 def timed_steps(step, steps, warmup, world, sync, dev):
@@ -313,7 +335,7 @@ def cifar_chain(args, world, rank, dev, gathered_classes=10, cpu=True):
     B, Hs = 256, 32
     chain = QConvChain(9, gathered_classes, args.quantizer, args.bits, args.precision, dev, seed=0)
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(200 + rank))).to(dev)
-    gathered = torch.empty(world * B, gathered_classes, device=dev) if world > 1 else None
+    gathered = gather_buffer(B, gathered_classes, dev)
     pack_batch = args.quantizer in ("po2", "po2+") and args.precision != "fp32"
     with torch.no_grad():
         for _ in range(2):  # autotune every shape + warm the caching allocator
@@ -332,7 +354,12 @@ def cifar_chain(args, world, rank, dev, gathered_classes=10, cpu=True):
         with torch.cuda.graph(graph):
             logits = chain.forward(x)
         gstep = lambda record=False: gather_logits(graph.replay() or logits, gathered, world)  # noqa: E731
-        dt = timed_steps(gstep, args.cifar_steps, 5, world, torch.cuda.synchronize, dev)
+        steps = leg_steps(gstep, args.cifar_steps, args.leg_seconds)
+        if world > 1:  # every rank times the same number of steps
+            t = torch.tensor([steps], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            steps = int(t.item())
+        dt = timed_steps(gstep, steps, 5, world, torch.cuda.synchronize, dev)
 
         def launch_ms(fn):  # average of 20 back-to-back launches captured in a graph, 5 replays
             fn()
@@ -390,14 +417,14 @@ def cifar_chain(args, world, rank, dev, gathered_classes=10, cpu=True):
                         "per-layer activations stay L2-resident inside the launch"}))
         cands.sort(key=lambda c: -c[0])
         roofline = cands[0][1]
-    images = world * B * args.cifar_steps
+    images = world * B * steps
     out = {"workload": "resnet56 quantized-conv chain @32x32 bs=%d per GPU: 56 fused %s-%dbit quantize+conv fwd "
                        "+ head, HIP graph replay%s" % (B, args.quantizer, args.bits,
                                                        " (each stage's stride-1 run of convs as one chain launch)"
                                                        if chain.chains else ""),
            "metric": "quantized-conv fwd images/sec, ResNet56 32x32 bs=256", "value": round(images / dt, 2),
-           "unit": "images/s", "n_gpus": world, "steps": args.cifar_steps, "ms_per_step": round(dt * 1e3 /
-                                                                                                args.cifar_steps, 4),
+           "unit": "images/s", "n_gpus": world, "steps": steps, "ms_per_step": round(dt * 1e3 / steps, 4),
+           "timed_seconds": round(dt, 3),
            "roofline": roofline, "cpu_baseline": None}
     if cpu:
         wcpu = [w.cpu() for w in chain.weights]
@@ -457,8 +484,13 @@ def model_extra(args, world, rank, dev, model_type, quantizer, bits, image, batc
                 graph.instantiate()
             except Exception:  # noqa: BLE001 -- already instantiated
                 pass
-        gathered = torch.empty(world * batch, classes, device=dev) if world > 1 else None
+        gathered = gather_buffer(batch, classes, dev)
         gstep = lambda record=False: gather_logits(graph.replay() or logits, gathered, world)  # noqa: E731
+        steps = leg_steps(gstep, steps, args.leg_seconds)
+        if world > 1:  # every rank times the same number of steps
+            t = torch.tensor([steps], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            steps = int(t.item())
         dt = timed_steps(gstep, steps, 5, world, torch.cuda.synchronize, dev)
         best = None
         for key, (cnt, w) in calls.items():
@@ -509,7 +541,7 @@ def model_extra(args, world, rank, dev, model_type, quantizer, bits, image, batc
                        "act + residual native), HIP graph replay" % (model_type, image, image, batch, quantizer, bits),
            "metric": "%s fwd images/sec, %s %dx%d bs=%d" % (label, model_type, image, image, batch),
            "value": round(images / dt, 2), "unit": "images/s", "n_gpus": world, "steps": steps,
-           "ms_per_step": round(step_ms, 4),
+           "ms_per_step": round(step_ms, 4), "timed_seconds": round(dt, 3),
            "roofline": {"scope": "step", "bound": "hbm", "achieved": round(step_achieved, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(step_achieved / PEAK_HBM_GBS, 4), "traffic": None,
                         "algorithmic_bytes_per_step": int(step_bytes), "flops_per_step": int(step_flops),
@@ -612,27 +644,42 @@ def launch_ranks(n, argv):
 
 
 def selftest(args, world, rank, backend):
-    """--selftest: the N-rank plumbing of the step without any kernel (CPU tensors, gloo): every rank's
-    batch shard of stand-in logits (a deterministic function of the rank), the all_gather of the
-    outputs and the barrier-bracketed max-over-ranks timing of timed_steps.  Rank 0 checks the gathered
-    logits against every shard and prints one JSON line (tests/test_distributed.py runs it through the
+    """--selftest: the N-rank step on the CPU over gloo, no kernels.  The global batch
+    (--global-batch, default 4 images per rank) is split evenly; every rank runs its contiguous shard
+    through the drop-in model's CPU path (ResNet20, po2 4-bit QAT-mode QuantizedConv2d layers: the
+    reference's torch arithmetic, bs / world images per rank, --image pixels), the logits are
+    all-gathered (gather_logits, the bench's collective) and the step is timed as timed_steps does
+    (barrier-bracketed, max over ranks).  Rank 0 checks the gathered logits against one unsharded
+    forward of the whole batch and prints one JSON line (tests/test_distributed.py runs it through the
     --gpus 2 entry)."""
-    B, classes = 4, 10
-    dev = torch.device("cpu")
+    from po2_quantization_amd.models.model import get_model
+    from po2_quantization_amd.utils.quantizers import quantizer_dict
 
-    def shard(r):
-        return torch.arange(B * classes, dtype=torch.float32).view(B, classes) * (r + 1) + 1000.0 * r
+    torch.set_num_threads(1)
+    total = args.global_batch if args.global_batch is not None else 4 * world
+    if total % world:
+        raise SystemExit("--global-batch %d is not divisible by the %d ranks" % (total, world))
+    B, classes, dev = total // world, 10, torch.device("cpu")
+    torch.manual_seed(0)  # identical weights on every rank, as the bench's seeded weights
+    m = get_model("resnet20", classes, quantizer_dict["po2"], 4, (args.image, args.image)).eval()
+    x_all = torch.randn(total, 3, args.image, args.image, generator=torch.Generator().manual_seed(1))
+    x = x_all[rank * B:(rank + 1) * B]
+    gathered = gather_buffer(B, classes, dev)
 
-    logits = shard(rank)
-    gathered = torch.empty(world * B, classes)
-    dt = timed_steps(lambda record=False: gather_logits(logits, gathered, world), args.steps, args.warmup, world,
-                     lambda: None, dev)
-    out = gather_logits(logits, gathered, world) if world > 1 else logits
-    expect = torch.cat([shard(r) for r in range(world)])
+    def step(record=False):
+        with torch.no_grad():
+            return gather_logits(m(x), gathered)
+
+    dt = timed_steps(step, args.steps, args.warmup, world, lambda: None, dev)
+    out = step()
     if rank == 0:
+        with torch.no_grad():
+            full = m(x_all)
+        err = float((out - full).abs().max() / full.abs().max())
         print(json.dumps({"selftest": True, "n_gpus": world, "world_size": world, "dist_backend": backend,
-                          "gathered_ok": bool(torch.equal(out, expect)), "gathered_rows": int(out.shape[0]),
-                          "steps": args.steps, "seconds": dt}), flush=True)
+                          "global_batch": total, "batch_per_rank": B, "gathered_rows": int(out.shape[0]),
+                          "gathered_err": err, "gathered_ok": err <= 1e-5, "steps": args.steps, "seconds": dt}),
+              flush=True)
 
 
 def main():
@@ -663,7 +710,10 @@ def main():
     ap.add_argument("--no-cifar", dest="cifar", action="store_false",
                     help="skip the config-2 line (ResNet56 @32x32 bs=256 chain from a HIP graph, "
                          "reported under config2_cifar32 next to the headline)")
-    ap.add_argument("--cifar-steps", type=int, default=200)
+    ap.add_argument("--cifar-steps", type=int, default=200, help="minimum timed steps of the config-2 leg")
+    ap.add_argument("--leg-seconds", type=float, default=5.0,
+                    help="the config-2/3/5 legs time at least this many seconds of GPU work (their step count "
+                         "grows to fit); the headline keeps exactly --steps")
     ap.add_argument("--no-models", dest="models", action="store_false",
                     help="skip the model-config lines (config 3: MobileNetV2 @32 po2+ 4-bit; config 5: MobileViT-XS "
                          "@256 po2+ 2-bit), reported under config3_mobilenet32 / config5_mobilevit256")
@@ -718,7 +768,7 @@ def main():
     chain.s2ds = not args.no_s2ds
     B, Hs = args.batch, args.image
     x = torch.relu(torch.randn(B, 16, Hs, Hs, generator=torch.Generator().manual_seed(100 + rank))).to(dev)
-    gathered = torch.empty(world * B, args.classes, device=dev) if world > 1 else None
+    gathered = gather_buffer(B, args.classes, dev)
 
     def step(record=False):
         return gather_logits(chain.forward(x, record), gathered, world)
@@ -871,9 +921,9 @@ def main():
         "layer_roofline": layer_roof,
         "cpu_baseline": None,
     }
-    # the CPU baselines run on rank 0 after each timed region (the other ranks wait at the next
-    # barrier), at every N
-    cpu_leg = rank == 0 and not args.no_cpu_baseline
+    # the CPU baselines run on rank 0 at N = 1 only: at N > 1 the other ranks would poll the next
+    # barrier beside it and skew the number
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline
     if cpu_leg:
         wcpu = [w.cpu() for w in chain.weights]
         out["cpu_baseline"] = cpu_baseline(chain.layers, wcpu, Hs, args.quantizer, args.bits, args.cpu_seconds)

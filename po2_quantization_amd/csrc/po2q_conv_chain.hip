@@ -225,8 +225,8 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     // residual loads are in flight, so the per-layer descriptor reads hit the scalar cache instead of
     // each paying a cold miss
     {
-        static_assert(offsetof(ChainArgs, layer) + sizeof(ChainLayer) * kChainMax + 16 <= 22 * 64 + 60,
-                      "the warm-up below covers 22 lines of kernel arguments");
+        static_assert(offsetof(ChainArgs, layer) + sizeof(ChainLayer) * kChainMax + 16 <= 22 * 64,
+                      "the warm-up below covers 22 whole 64-byte lines of kernel arguments");
         const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
         unsigned d;
 #define PO2Q_WL(o) "s_load_dword %0, %1, " #o "\n\t"

@@ -307,10 +307,11 @@ struct PackJob {
     int lo, hi, mode, nb, plain, nparts;
     PackX3 pg;
 };
-constexpr int kPackBatch = 36;  // 36 x 104-byte jobs: 3.7 KB of kernel arguments (the limit is 4 KB)
+constexpr int kPackBatch = 36;  // 36 x 112-byte jobs: 3.9 KB of kernel arguments (the limit is 4 KB)
 struct PackBatch {
     PackJob job[kPackBatch];
 };
+static_assert(sizeof(PackBatch) <= 4096, "pack_batch_kernel's arguments must fit the 4 KB kernel-argument limit");
 
 // The absmax of the batch's larger tensors as its own launch in front of pack_batch_kernel: block
 // (c, layer) reduces chunk c (kAbsChunk elements: one float4 per thread x 4 in flight) into
@@ -327,6 +328,7 @@ struct AbsJob {
 struct AbsBatch {
     AbsJob job[kPackBatch];
 };
+static_assert(sizeof(AbsBatch) <= 4096, "absmax_batch_kernel's arguments must fit the 4 KB kernel-argument limit");
 __global__ __launch_bounds__(256) void absmax_batch_kernel(AbsBatch B) {
     const AbsJob& j = B.job[blockIdx.y];
     if ((int)blockIdx.x >= j.nparts) return;  // block-uniform

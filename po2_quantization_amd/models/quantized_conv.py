@@ -29,6 +29,7 @@ sequence unchanged.
 import contextlib
 import os
 import threading
+import weakref
 
 import torch
 import torch.nn as nn
@@ -261,6 +262,10 @@ def _side_stream(device):
     return s
 
 
+# model -> {forward key: recorded layers}; weak, so a dropped model takes its records with it
+_RECORDS = weakref.WeakKeyDictionary()
+
+
 @contextlib.contextmanager
 def batched_packs(model, x):
     """Run a model's eval forward with its single-conv layers' weight packs batched (BATCHED_PACKS)."""
@@ -273,7 +278,9 @@ def batched_packs(model, x):
     confs = tuple((m.bits, NATIVE_MODES.get(m.quantize_fn), m.precision) for m in model.modules()
                   if isinstance(m, QuantizedConv2d))
     key = (tuple(x.shape), x.device, INFERENCE_FUSION, IR_FUSION, confs)
-    rec = model.__dict__.setdefault("_po2q_packs", {})
+    rec = _RECORDS.get(model)
+    if rec is None:  # keyed by the model object itself: DataParallel replicas (shallow __dict__ copies) get their own
+        rec = _RECORDS[model] = {}
     sess = _ForwardPacks(model, rec.get(key))
     _tls.packs = sess
     try:

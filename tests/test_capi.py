@@ -84,9 +84,10 @@ def test_workspace_sizes_are_small(shape):
         assert 0 < nbytes < 64 * K * max(Cg, 4) * R * S + 65536
 
 
-def test_cpu_conv_raises_quantizer_restated():
-    """The conv has no CPU path (raises); the PO2 quantizers take CPU tensors through the
-    product-side torch restatement, never through the oracle."""
+def test_cpu_conv_torch_path_quantizer_restated():
+    """CPU tensors: the conv runs the reference's torch arithmetic (F.conv2d of the restated Q(w)) and the
+    PO2 quantizers the product-side torch restatement, never the oracle; a HIP conv input
+    that is not fp32 still raises (no silent fallback on the device)."""
     import torch
 
     from po2_quantization_amd.models.quantized_conv import QuantizedConv2d
@@ -98,8 +99,11 @@ def test_cpu_conv_raises_quantizer_restated():
     assert torch.equal(y, _lib.restated_quantize(w, 4, "po2"))
     assert torch.equal(quantizer_dict["po2+"].forward(None, w, bits=3), _lib.restated_quantize(w, 3, "po2+"))
     conv = QuantizedConv2d(4, 4, 3, quantize_fn=PowerOfTwoQuantizer, bits=4)
+    x = torch.randn(1, 4, 8, 8)
+    ref = torch.nn.functional.conv2d(x, _lib.restated_quantize(conv.weight.detach(), 4, "po2"), None, 1, 1)
+    assert torch.equal(conv(x).detach(), ref)
     with pytest.raises(RuntimeError, match="HIP device"):
-        conv(torch.randn(1, 4, 8, 8))
+        _lib.qconv2d(x, conv.weight.detach(), None, 1, 1, 1, 1, 4, "po2")
 
 
 def test_bf16x3_eligibility_on_host():

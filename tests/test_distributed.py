@@ -13,6 +13,10 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from po2_quantization_amd import qat
+from po2_quantization_amd.models.model import get_model
+from po2_quantization_amd.utils.quantizers import quantizer_dict
+
 
 def _free_port():
     with socket.socket() as s:
@@ -122,6 +126,29 @@ def test_bench_entry_starts_n_ranks():
     assert out["gathered_ok"] and out["gathered_rows"] == 8, out
 
 
+def test_bench_entry_global_batch_1024_split():
+    """Config 4's split (--global-batch 1024 over the ranks, reference README.md:42 / train.py:25-26) through
+    the --gpus 2 entry: each rank runs its 512-image shard through the drop-in ResNet20's QuantizedConv2d
+    layers (CPU path, po2 4-bit), the logits are all-gathered over gloo, and rank 0 finds them equal to one
+    unsharded forward of all 1024 images."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--selftest", "--steps", "2",
+                        "--warmup", "1", "--global-batch", "1024", "--image", "8"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["global_batch"] == 1024 and out["batch_per_rank"] == 512 and out["gathered_rows"] == 1024, out
+    assert out["gathered_ok"], out
+
+
 def test_bench_entry_rejects_world_mismatch():
     """Under an external launcher the process group must hold exactly --gpus ranks."""
     import subprocess
@@ -136,3 +163,59 @@ def test_bench_entry_rejects_world_mismatch():
 
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
+
+
+def _gradsync_worker(rank, world, port, out):
+    """The same 3 training steps twice from per-rank initial weights: through DDP (the reference's wrapper)
+    and through the plain module of build_model(..., ddp=False) with qat.GradSync (the collectives
+    GraphedTrainStep captures)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    dev = torch.device("cpu")
+    g = torch.Generator().manual_seed(9)
+    images = torch.randn(24, 3, 16, 16, generator=g)
+    labels = torch.randint(0, 10, (24,), generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+    res = []
+    for use_sync in (False, True):
+        torch.manual_seed(rank)  # different initial weights per rank: the construction broadcast aligns them
+        m = qat.build_model("resnet20", 10, quantizer_dict["po2"], 4, (16, 16), dev, sync_bn=False, ddp=not use_sync)
+        core = m.module if hasattr(m, "module") else m
+        if rank == 1:  # per-rank BN statistics: the buffer broadcast must make rank 0's win
+            with torch.no_grad():
+                for b in core.buffers():
+                    if b.is_floating_point():
+                        b.add_(0.25)
+        sync = qat.GradSync(m) if use_sync else None
+        opt, _, _, _ = qat.make_optimizer(m, 0.01, 10)
+        for x, y in qat.shard_batches(images, labels, 4, epoch=0):
+            qat.train_step(m, opt, crit, x, y, sync)
+        res.append(torch.cat([t.detach().double().flatten() for t in core.parameters()] +
+                             [t.detach().double().flatten() for t in core.buffers()]))
+    flat = torch.stack(res)
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    torch.distributed.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save(torch.stack(gathered), out)
+    torch.distributed.destroy_process_group()
+
+
+def test_gradsync_equals_ddp_two_ranks(tmp_path):
+    """GradSync (coalesced rank-0 buffer broadcast + averaged-gradient all_reduce, capturable in a HIP
+    graph) reproduces DistributedDataParallel's training steps bit for bit over 2 gloo ranks, the reference's
+    DDP step (train.py:79-94, 153-155) on the CPU path of the drop-in convs."""
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "state.pt")
+    mp.spawn(_gradsync_worker, args=(2, port, out), nprocs=2, join=True)
+    p = torch.load(out, weights_only=True)  # [rank][ddp | gradsync][parameters, buffers]
+    n = sum(t.numel() for t in get_model("resnet20", 10, None, 4, (16, 16)).parameters())
+    # parameters in lock-step on both routes (the buffers hold each rank's last local BN update)
+    assert torch.equal(p[0, 0, :n], p[1, 0, :n]) and torch.equal(p[0, 1, :n], p[1, 1, :n])
+    for r in range(2):  # and each rank's whole state equal between DDP and GradSync
+        assert torch.equal(p[r, 0], p[r, 1]), (r, (p[r, 0] - p[r, 1]).abs().max())

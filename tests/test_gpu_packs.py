@@ -169,3 +169,37 @@ def test_side_stream_packs_ordered_and_graph_capturable(name, image, monkeypatch
             g.replay()
             torch.cuda.synchronize()
             assert torch.equal(out, ref2)
+
+
+def test_replica_records_its_own_packs(monkeypatch):
+    """A DataParallel-style replica (torch.nn.parallel.replicate: new module objects made from a shallow
+    copy of the original's attributes) keeps its own layer record: its first forward records
+    its own layers, and from its second forward on every layer that reads a pack in the original model's
+    forwards reads one from the replica's own batched launch (the lookups key on the replica's modules)."""
+    monkeypatch.setattr(qc, "IR_FUSION", False)
+    torch.manual_seed(6)
+    m = get_model("resnet20", 10, quantizer_dict["po2"], 4, (64, 64)).to(DEV).eval()
+    x = torch.randn(2, 3, 64, 64, device=DEV)
+    calls = []
+    real_packed = _lib.qconv2d_packed
+
+    def spy_packed(*a, **k):
+        calls.append(1)
+        return real_packed(*a, **k)
+
+    monkeypatch.setattr(_lib, "qconv2d_packed", spy_packed)
+    with torch.no_grad():
+        m(x)
+        del calls[:]
+        ref = m(x)
+        n_orig = len(calls)
+        rep = torch.nn.parallel.replicate(m, [0], detach=True)[0]
+        assert rep is not m
+        del calls[:]
+        y1 = rep(x)  # records the replica's layers
+        n_first = len(calls)
+        del calls[:]
+        y2 = rep(x)  # reads its own batched packs
+        n_second = len(calls)
+    assert n_orig > 0 and n_first == 0 and n_second == n_orig, (n_orig, n_first, n_second)
+    assert torch.equal(y1, ref) and torch.equal(y2, ref)

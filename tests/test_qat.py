@@ -172,3 +172,4 @@ def _graphed_vs_eager():
     first = gs.graph
     gs.step(*batches[0])
     assert gs.graph is not first
+
