@@ -1391,6 +1391,16 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         po2q::set_error("po2q: pair: y must not alias x or the residual");
         return PO2Q_ERR_INVALID;
     }
+    if (po2q::pairw_applicable(N, C, H, W)) {  // stage 2 @112: 4 waves x 32 columns (po2q_conv_pairw.hip)
+        const hipError_t e = po2q::pairw_launch(x, w1, w2, y, N, H, W, bits, fsr, mode, bias1, bias2, post_scale1,
+                                                post_shift1, act1, post_scale2, post_shift2, residual, act2,
+                                                reinterpret_cast<hipStream_t>(stream));
+        if (e != hipSuccess) {
+            po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));
+            return PO2Q_ERR_HIP;
+        }
+        return PO2Q_OK;
+    }
     po2q::PairPlan pp;
     int pd, nts, prio, halves, stg;
     pair_variant(pd, nts, prio, halves, stg, C);

@@ -214,6 +214,14 @@ hipError_t launch_conv_ir(const IrPlan& ip, const float* x, float* y, int N, int
                           int S, const uint16_t* we, const float* we_scale, const float* wd, const uint16_t* wp,
                           const float* wp_scale, const IrEpi& e, hipStream_t s);
 
+// The stage-2 conv pair (C = 32, 96 < W <= 128) as 4 waves x 32 columns with every weight in VGPRs
+// (po2q_conv_pairw.hip); po2q_qconv2d_pair_f32 routes the shapes it takes there.
+bool pairw_applicable(int64_t N, int64_t C, int64_t H, int64_t W);
+hipError_t pairw_launch(const float* x, const float* w1, const float* w2, float* y, int64_t N, int64_t H,
+                        int64_t W, int bits, int fsr, int mode, const float* bias1, const float* bias2,
+                        const float* post_scale1, const float* post_shift1, int act1, const float* post_scale2,
+                        const float* post_shift2, const float* residual, int act2, hipStream_t s);
+
 // fp64 / bf16 (bit patterns) PO2 / PO2+ quantizer (po2q_quant_dtypes.hip): absmax partials
 // (nparts = absmax_blocks(n) uint64 words), then the quantize pass.
 template <typename T>

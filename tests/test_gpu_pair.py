@@ -235,3 +235,29 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     if C == 16 and W > 192 and pd == 5:  # 7-wave widths: with PO2Q_PAIR_MW unset the default is MW at PD 5
         monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
         assert torch.equal(_lib.qconv2d_pair(x, w1, w2, 4, "po2"), outs[0])
+
+
+@pytest.mark.parametrize("shape", [(2, 23, 112, 32), (1, 112, 112, 32), (3, 9, 100, 32), (2, 1, 104, 32),
+                                   (4, 13, 108, 32)])
+def test_pair_w32_bitwise_equal_7wave_kernel(shape, monkeypatch):
+    """Stage 2's 4-wave kernel (po2q_conv_pairw.hip: 32 columns per wave, both convs' weights in VGPRs,
+    whole-line stores; the default for C = 32 at 96 < W <= 128) runs the 7-wave conv_pair<32>'s
+    arithmetic -- the same fragments, the same MFMA order per accumulator, the same epilogue expressions
+    -- so its output is bit for bit the 7-wave kernel's (PO2Q_PAIR_W32=0) in the plain, general and
+    BasicBlock forms, at both ring depths of the plain form; ragged widths and 1-row images included."""
+    N, H, W, C = shape
+    x, w1, w2, e = make(N, H, W, 51 + W + H, True, C)
+    g = torch.Generator().manual_seed(W)
+    b1, b2 = (torch.randn(C, generator=g) * 0.1).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    forms = [{}, dict(act1="relu", act2="relu6", **e), dict(act1="relu", act2="relu", residual=x, **e),
+             dict(act1="silu", act2="relu", residual=x.flip(3).contiguous(), bias1=b1, bias2=b2, **e)]
+    for kw in forms:
+        monkeypatch.setenv("PO2Q_PAIR_W32", "0")
+        ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", **kw)
+        for knob in (("2", "3") if not kw else ("2",)):
+            monkeypatch.setenv("PO2Q_PAIR_W32", knob)
+            y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", **kw)
+            assert torch.equal(y, ref), (shape, knob, sorted(kw), nerr(y, ref))
+    t = torch_chain(x, w1, w2, e, "relu", "relu", x, "po2+")
+    monkeypatch.delenv("PO2Q_PAIR_W32", raising=False)
+    assert nerr(_lib.qconv2d_pair(x, w1, w2, 4, "po2+", **forms[2]), t) <= CONV_TOL

@@ -20,7 +20,9 @@ def main():
     i64, i32, p = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
     L.po2q_qconv2d_pair_f32.argtypes = [p, p, p, p, i64, i64, i64, i64, i32, i32, i32, p, p, p, p, i32, p, p, p, i32, p]
     L.po2q_qconv2d_pair_f32.restype = i32
-    N, C, H = 256, 16, 224
+    N = 256
+    C = int(os.environ.get("PAIR_C", "16"))
+    H = 224 if C == 16 else 112
     dev = torch.device("cuda:0")
     x = torch.relu(torch.randn(N, C, H, H, device=dev))
     w1 = torch.randn(C, C, 3, 3, device=dev) * 0.1
@@ -33,7 +35,8 @@ def main():
                                      torch.cuda.current_stream().cuda_stream)
         assert st == 0, st
 
-    os.environ["PO2Q_PAIR_VARIANT"] = "23"
+    if C == 16:
+        os.environ["PO2Q_PAIR_VARIANT"] = "23"
     vals = [v for v in os.environ.get("PAIR_DBG", "0,3,4,8,12,16,19,15,31").split(",")]
     ts = {}
     for _ in range(3):
@@ -42,7 +45,7 @@ def main():
             ts.setdefault(v, []).append(timeit(call, 7))
     out = {k: round(sorted(t)[len(t) // 2], 4) for k, t in ts.items()}
     out["copy_in_bytes_ms"] = round(timeit(lambda: y.copy_(x), 7), 4)
-    print(json.dumps({"pair_ablation_ms": out, "bits": "1 no conv2 MFMA, 2 no conv1 MFMA, 4 no x DMA, "
+    print(json.dumps({"C": C, "pair_ablation_ms": out, "bits": "1 no conv2 MFMA, 2 no conv1 MFMA, 4 no x DMA, "
                       "8 no stores, 16 no split/epi1 writes"}), flush=True)
 
 
