@@ -64,8 +64,6 @@ struct PairArgs {
     int act1, act2;
     const float* res;  // RES: residual [N, C, H, W] added before act2
     int prio;          // 1: the second wave of each SIMD (waves 4..) issues at priority 1
-    int halves;        // unused (the half-line A/B knob of round 2: C = 16 always stores whole lines)
-    int stg;           // 1: the stagger (STG) kernel for the forms without a residual
     unsigned* stamps;  // PO2Q_PAIR_STAMPS diagnostic builds only: per-wave phase cycle sums
     int mw;            // 1: the memory-wave kernel (MW) where it applies
 };
@@ -126,11 +124,9 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // general epilogues, 2 = the BasicBlock form (ReLU after both BNs: the conv scale and bias folded
 // into the BN affine at staging, a compile-time ReLU; the kernel is bound by vector-instruction
 // issue, so the common forms skip that work).
-// STG 1 (stagger, MI355X_MICROARCH "two waves per SIMD" item 9): waves 4.. -- the second wave
-// of each SIMD -- run a step's conv-2 epilogue at the start of the NEXT step and split x row j
-// before their conv-2 MFMAs, so right after the barrier they issue vector work while waves
-// 0-3 issue matrix work, instead of both waves of a SIMD contending for the matrix pipe and
-// then both idling it.  Outputs are bit for bit those of STG 0 (same arithmetic, moved).
+// (Measured off and removed in round 6, numbers in DESIGN.md: the stagger kernel -- waves 4.. one
+// epilogue late --, packed-fp32 splits, conv 2's tap-row-0 weights in VGPRs at C = 32, a one-k-step
+// fragment prefetch, temporal C = 32 stores, and the role-split kernel conv_pair_ab.)
 // DBG (diagnostic builds only, -DPO2Q_PAIR_DIAG, PO2Q_PAIR_DEBUG; timing only, outputs are
 // wrong): bit 1 no conv-2 MFMAs, 2 no conv-1 MFMAs, 4 no x DMAs, 8 no output stores, 16 no
 // split / epilogue-1 plane writes.
@@ -140,22 +136,9 @@ __device__ __forceinline__ int xa(int hp, int oc) {
 // its own x DMA of the previous step AND every store issued before it.  Plain / general forms
 // without a residual, seven compute waves (C = 16: 192 < W <= 224, C = 32: 96 < W <= 112); a row is
 // 14 DMA instructions either way (C x 7 * 512 / C / 4 float4).
-// Packed fp32 (v_pk_fma / v_pk_add) in this kernel's exact splits and plain epilogues: off by
-// default -- same IEEE results, fewer VALU instructions, but the kernel measured 2-4 % slower
-// with them (same-box A/B, profiles/r04_pair_packed_ab.jsonl); -DPO2Q_PAIR_PK=1 builds them.
-#ifndef PO2Q_PAIR_PK
-#define PO2Q_PAIR_PK 0
-#endif
-#ifndef PO2Q_PAIR_W2R
-#define PO2Q_PAIR_W2R 0
-#endif
-constexpr bool kPairPK = PO2Q_PAIR_PK != 0;
-
-template <int CC, int PD, int NTS, bool RES, int E = 1, int STG = 0, int DBG = 0, int MW = 0>
+template <int CC, int PD, int NTS, bool RES, int E = 1, int DBG = 0, int MW = 0>
 __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x, float* __restrict__ y,
                                                     PairArgs a) {
-    static_assert(!(STG && RES), "stagger: the residual row's LDS slot is refilled before a deferred epilogue");
-    static_assert(!MW || !STG, "memory wave: no stagger");
     // MW with RES: the residual IS x (the BasicBlock's identity shortcut, checked on the host) and is
     // read from the x ring itself: raw row r is split at step r and re-read as output row r - 2's
     // residual at step r + 3, so the ring keeps 4 rows behind the current one (MWL = 4) -- no
@@ -308,11 +291,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     float scale1 = 1.0f, scale2 = 1.0f;
     bool fin1 = true, fin2 = true;
     bf16x8 bw1[NF], bw2[WL2 ? 1 : NF];
-    // C = 32, -DPO2Q_PAIR_W2R=1: conv 2's tap-row-0 B fragments also in VGPRs (the rest stay in
-    // LDS), a third fewer LDS weight reads per step.  Off: 0.353 vs 0.343 ms for the stage-2 pair and
-    // 2 % fewer images/s in the bench with it (226 VGPRs; profiles/r04_pair32_w2r_ab.jsonl)
-    constexpr int W2R = WL2 ? PO2Q_PAIR_W2R : 0;
-    bf16x8 bw2r[W2R ? KS * NT : 1];
     float bk1[E ? NT * 4 : 1], e1s[E ? NT * 4 : 1], e1b[E ? NT * 4 : 1];  // conv 1: ch 16 nt + 4 (lane >> 4) + e
     float bk2[NT], e2s[NT], e2b[NT];                                       // conv 2: ch 16 nt + (lane & 15)
     floatx4 acc1[3][NG][NT], acc2[3][NG][NT];
@@ -328,25 +306,10 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     // 3 tap rows x KS k-steps x 3 planes x NG groups x NT tiles of MFMAs on one split row
     // into accumulator slots SL.  TR (conv 1): transposed (A = weights), x planes, VGPR
     // weights; else (conv 2): shared planes (two b64 per fragment), weights per WL2
-    // PF (conv 2, -DPO2Q_PAIR_PF=1; off): the fragments of k-step ks + 1 (A from the shared planes; B
-    // from LDS at C = 32) read before the MFMAs of k-step ks, into a second register set, pinned there
-    // by a sched_barrier (the compiler issues each read one or two MFMA groups before its use).  Waits
-    // per C = 32 step 33 -> 22 and the conv-2 phase 2402 -> 2186 cycles in the stamps build, but the
-    // product kernels did not get faster: C = 32 plain 0.362 vs 0.351 ms, and the C = 32 BasicBlock
-    // form ran out of VGPRs (0.637 vs 0.380 ms), same box (profiles/r05_pair_pf_ab.jsonl).  The conv-2
-    // phase is long because it is the phase right after the barrier, where both waves of a SIMD issue
-    // MFMAs at once (2 x 54 x 16 cycles), not because of the read latency.
-#ifndef PO2Q_PAIR_PF
-#define PO2Q_PAIR_PF 0
-#endif
-    // 3 tap rows x KS k-steps x 3 planes x NG groups x NT tiles of MFMAs on one split row
-    // into accumulator slots SL.  TR (conv 1): transposed (A = weights), x planes, VGPR
-    // weights; else (conv 2): shared planes (two b64 per fragment), weights per WL2
     auto mfmas = [&](auto S_, auto TR_, floatx4 (&acc)[3][NG][NT], const bf16x8 (&bw)[NF],
                      const bf16x8 (&bw2v)[WL2 ? 1 : NF], const unsigned char* pb) __attribute__((always_inline)) {
         constexpr int SR = decltype(S_)::value;
         constexpr bool TR = decltype(TR_)::value;
-        constexpr bool PF = !TR && PO2Q_PAIR_PF != 0;
         constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
         // fragments of k-step ks: the 3 planes, or for C = 16's k-step 1 the two paired ones; at
         // C = 32 (conv 2) also the 3 x NT B fragments of the k-step from LDS
@@ -374,8 +337,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                     const int f = (rr * KS + ks) * NT + nt;
                     if constexpr (TR)
                         bf[r3][nt] = bw[f];
-                    else if (WL2 && W2R && rr == 0)
-                        bf[r3][nt] = bw2r[W2R ? f : 0];
                     else if constexpr (WL2)
                         bf[r3][nt] = __builtin_bit_cast(bf16x8, wl2[f * 64 + lane]);
                     else
@@ -406,29 +367,12 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                         }
                 }
         };
-        if constexpr (PF) {
-            bf16x8 af[2][3][NG], bf[2][3][NT];
-            load_a(0, af[0]);
-            load_b(0, bf[0]);
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                if (ks + 1 < KS) {
-                    load_a(ks + 1, af[(ks + 1) & 1]);
-                    load_b(ks + 1, bf[(ks + 1) & 1]);
-                    // pins the reads above this k-step's MFMAs (the scheduler otherwise sinks each to
-                    // just before its use); the waits stay counted (lgkmcnt(N)) before each MFMA group
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                mma(ks, af[ks & 1], bf[ks & 1]);
-            }
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                bf16x8 af[3][NG], bf[3][NT];
-                load_a(ks, af);
-                load_b(ks, bf);
-                mma(ks, af, bf);
-            }
+        for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 af[3][NG], bf[3][NT];
+            load_a(ks, af);
+            load_b(ks, bf);
+            mma(ks, af, bf);
         }
     };
 
@@ -452,19 +396,11 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             for (int grp = 0; grp < NG; ++grp) {
                 const int ql = 16 * grp + 4 * g;  // strip column of the lane's 4 pixels
                 floatx4 v;
-                if constexpr ((E == 0 || E == 2) && kPairPK) {  // one fma per value, as packed v_pk_fma_f32 pairs
-                    const float sm = E == 0 ? scale2 : e2s[nt], ad = E == 0 ? 0.0f : e2b[nt];  // E 2: folded
-                    const po2q_float2 s2 = {sm, sm}, b2 = {ad, ad};
-                    const po2q_float2 v01 = po2q_float2{acc2[D][grp][nt][0], acc2[D][grp][nt][1]} * s2 + b2;
-                    const po2q_float2 v23 = po2q_float2{acc2[D][grp][nt][2], acc2[D][grp][nt][3]} * s2 + b2;
-                    v = floatx4{v01.x, v01.y, v23.x, v23.y};
-                } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
-                               : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
-                                        : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
-                }
+                for (int e = 0; e < 4; ++e)
+                    v[e] = E == 0 ? acc2[D][grp][nt][e] * scale2 + 0.0f
+                           : E == 2 ? acc2[D][grp][nt][e] * e2s[nt] + e2b[nt]  // folded: scale2 * ps2, b2 * ps2 + pb2
+                                    : (acc2[D][grp][nt][e] * scale2 + bk2[nt]) * e2s[nt] + e2b[nt];
                 if constexpr (RES) {
                     const floatx4 r = MW ? *reinterpret_cast<const floatx4*>(rres_ring + ch * RPB + ql * 4)
                                          : *reinterpret_cast<const floatx4*>(rres_row + ch * (SW * 4) + ql * 4);
@@ -521,7 +457,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     auto split_x = [&](const uint32_t (&bx)[8], uint32_t hx) __attribute__((always_inline)) {
         if constexpr ((DBG & 16) != 0) return;
         uint4 hi, mid, lo;
-        split3<kPairPK>(bx, hi, mid, lo);
+        split3<false>(bx, hi, mid, lo);
         *reinterpret_cast<uint4*>(slab + wa_i) = hi;
         *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
         *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
@@ -535,8 +471,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     };
 
     const bool strip_full = q0 + SW <= a.W;  // wave-uniform
-    // the stagger's late waves (wave-uniform: an SGPR branch)
-    const bool late = STG != 0 && wave >= 4;
 #ifdef PO2Q_PAIR_STAMPS
     unsigned ph_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev_ = 0;
@@ -563,12 +497,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * RPB);
             hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
         }
-        if constexpr (STG != 0) {
-            if (late) {  // vector work first: the previous step's conv-2 epilogue, then the x split
-                epi2(std::integral_constant<int, (S6 + 5) % 6>{}, j - 1);
-                split_x(bx, hx);
-            }
-        }
 
         // ---- conv 2 on intermediate row i = j - 3 (its halo index), straight from the shared planes
         // (unconditional: in steps 0-2 it reads the zeroed ring slots and its outputs are dropped --
@@ -576,12 +504,10 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         if constexpr ((DBG & 1) == 0)
             mfmas(std::integral_constant<int, S>{}, std::false_type{}, acc2, bw1, bw2, yr + YR * yslot);
         PO2Q_PSTAMP(3);
-        if (!late) {
-            epi2(S_, j);
-            PO2Q_PSTAMP(4);
-            split_x(bx, hx);
-            PO2Q_PSTAMP(5);
-        }
+        epi2(S_, j);
+        PO2Q_PSTAMP(4);
+        split_x(bx, hx);
+        PO2Q_PSTAMP(5);
 
         // ---- conv 1 on x row j (transposed MFMAs); intermediate row i = j - 2 completes
         if constexpr ((DBG & 2) == 0) mfmas(std::integral_constant<int, S>{}, std::true_type{}, acc1, bw1, bw2, slab);
@@ -601,30 +527,20 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
                     uint32_t b4[4];
-                    if constexpr (E == 0 && kPairPK) {  // packed v_pk_fma_f32 pairs (the same fma per value)
-                        const po2q_float2 s1 = {scale1, scale1}, z = {0.0f, 0.0f};
-                        const po2q_float2 t01 = po2q_float2{acc1[D][grp][nt][0], acc1[D][grp][nt][1]} * s1 + z;
-                        const po2q_float2 t23 = po2q_float2{acc1[D][grp][nt][2], acc1[D][grp][nt][3]} * s1 + z;
-                        b4[0] = __float_as_uint(t01.x);
-                        b4[1] = __float_as_uint(t01.y);
-                        b4[2] = __float_as_uint(t23.x);
-                        b4[3] = __float_as_uint(t23.y);
-                    } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            float t;
-                            if constexpr (E == 0) {
-                                t = acc1[D][grp][nt][e] * scale1 + 0.0f;
-                            } else if constexpr (E == 2) {
-                                const int c = nt * 4 + e;
-                                t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
-                                t = t < 0.0f ? 0.0f : t;
-                            } else {
-                                const int c = nt * 4 + e;
-                                t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
-                            }
-                            b4[e] = __float_as_uint(t);
+                    for (int e = 0; e < 4; ++e) {
+                        float t;
+                        if constexpr (E == 0) {
+                            t = acc1[D][grp][nt][e] * scale1 + 0.0f;
+                        } else if constexpr (E == 2) {
+                            const int c = nt * 4 + e;
+                            t = acc1[D][grp][nt][e] * e1s[c] + e1b[c];  // folded affine, then ReLU
+                            t = t < 0.0f ? 0.0f : t;
+                        } else {
+                            const int c = nt * 4 + e;
+                            t = epi_act((acc1[D][grp][nt][e] * scale1 + bk1[c]) * e1s[c] + e1b[c], a.act1);
                         }
+                        b4[e] = __float_as_uint(t);
                     }
                     if (!allok) {  // wave-uniform: only rows / strips that leave the image pay the select
                         const bool ok = irow && q < a.W;
@@ -632,7 +548,7 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
                         for (int e = 0; e < 4; ++e) b4[e] = ok ? b4[e] : 0u;
                     }
                     uint2 h2, m2, l2;
-                    split4p<kPairPK>(b4, h2, m2, l2);
+                    split4p<false>(b4, h2, m2, l2);
                     const int wo = yoct<CC>(q + 1, (4 * nt + g) >> 1) + 8 * (g & 1);
                     *reinterpret_cast<uint2*>(yw + wo) = h2;
                     *reinterpret_cast<uint2*>(yw + YPL + wo) = m2;
@@ -695,11 +611,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         scale2 = wq_prologue(a.q2, thr, red, nw + MW, fin2);
         if constexpr (WL2) {
             for (int e = tid; e < NF * 64; e += blockDim.x) wl2[e] = wq_frag_rows(a.q2, CC, CC, CC, NT, KS, e, scale2, fin2, thr);
-            if constexpr (W2R != 0) {
-#pragma unroll
-                for (int f = 0; f < KS * NT; ++f)
-                    bw2r[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
-            }
         } else {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
@@ -736,10 +647,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
         if constexpr (!WL2) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw2[WL2 ? 0 : f]));
-        }
-        if constexpr (W2R != 0) {
-#pragma unroll
-            for (int f = 0; f < KS * NT; ++f) asm volatile("" : "+v"(bw2r[W2R ? f : 0]));
         }
         if constexpr (E == 2) {  // BasicBlock form: the conv scale and bias folded into the affine
 #pragma unroll
@@ -790,20 +697,14 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
             return;
         }
     }
-    int jl = 0;  // the last step run (its S6 is 2 or 5: both complete accumulator slot 1)
     for (int j = 0; j < nsteps; j += 6) {
         step(std::integral_constant<int, 0>{}, j);
         step(std::integral_constant<int, 1>{}, j + 1);
         step(std::integral_constant<int, 2>{}, j + 2);
-        jl = j + 2;
         if (j + 3 >= nsteps) break;
         step(std::integral_constant<int, 3>{}, j + 3);
         step(std::integral_constant<int, 4>{}, j + 4);
         step(std::integral_constant<int, 5>{}, j + 5);
-        jl = j + 5;
-    }
-    if constexpr (STG != 0) {
-        if (late) epi2(std::integral_constant<int, 2>{}, jl);  // the deferred last epilogue
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the wave ends
 #ifdef PO2Q_PAIR_STAMPS
@@ -812,333 +713,6 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
 #endif
 }
 
-
-// ------------------------------------------------------------- role-split pair --
-// conv_pair_ab: the same C = 16 BasicBlock chain as conv_pair with the two convs given to
-// different waves.  8 waves (W <= 256: 2 x ceil(W / 64)): waves 0 .. NR-1 ("A") own 64 output
-// columns each of conv 1 -- x DMA, exact split, 72 transposed MFMAs per step, and the epilogue-1
-// split of the intermediate row into the shared planes; waves NR .. 2 NR - 1 ("B") own the same
-// columns of conv 2 -- 72 MFMAs on the shared planes, epilogue 2, the output stores.  A block's
-// waves go to the SIMDs in a cyclic order, so wave w and wave w + 4 share a SIMD: each SIMD pairs
-// an A wave with a B wave.  Why: in conv_pair every wave runs conv 2 then conv 1 behind one
-// barrier, so the two waves of a SIMD issue their MFMAs, then their VALU splits, at the same
-// time (tools/pair_ablate.py: compute alone 0.39 ms, memory alone 0.36 ms, together 0.56 ms).
-// Here A opens each step with VALU (the deferred epilogue 1 of the row completed one step
-// earlier, then the split of x) while B opens with MFMAs, and A's MFMAs run beside B's epilogue
-// and stores.  Deferring epilogue 1 by one step makes B lag conv_pair's conv 2 by one row:
-// step j: A splits x row j, conv 1 -> intermediate row j - 2 completes (epilogue at step j + 1);
-//         B: conv 2 on intermediate row j - 4 (written at step j - 1), output row j - 6.
-// Arithmetic identical to conv_pair (same splits, same MFMA order per accumulator).
-constexpr int kABSW = 64;                        // output columns per wave (4 x 16-pixel groups)
-constexpr int kABPlane = (kABSW + 2) * 32 + 32;  // a wave's x planes: [66 px][16 ch] bf16 + zero slot
-
-struct PairABArgs {
-    int N, H, W;
-    int Wp;   // 64 x NR
-    int YPL;  // bytes of one shared intermediate plane: (Wp + 3) px x 32 B
-    int RB, nseg, items, remap;
-    int NR;   // waves per role
-    WQuant q1, q2;
-    const float* b1;
-    const float* b2;
-    const float* ps1;
-    const float* pb1;
-    const float* ps2;
-    const float* pb2;
-    int act1, act2;
-};
-
-template <int E>
-__global__ __launch_bounds__(512, 1) void conv_pair_ab(const float* __restrict__ x, float* __restrict__ y,
-                                                       PairABArgs a) {
-    constexpr int CC = 16, SW = kABSW, WC = SW + 2, PL = kABPlane, KS = 2, NG = SW / 16, NF = 3 * KS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nw = (int)(blockDim.x >> 6);
-    const int NR = a.NR;
-    const bool isA = wave < NR;  // wave-uniform
-    const int wr = isA ? wave : wave - NR;
-    const int rawslot = CC * a.Wp * 4;
-    const int yslot = 3 * a.YPL;
-    unsigned char* raw = lds;                                 // 2 x [16][Wp] fp32 (x rows)
-    unsigned char* yr = raw + 2 * rawslot;                    // 2 x 3 planes (intermediate)
-    unsigned char* slab = yr + 2 * yslot + wr * (3 * PL);     // A: this wave's x planes
-    const int zero_off = WC * CC * 2;
-    const int yzero = (a.Wp + 2) * (2 * CC);
-
-    int blk = blockIdx.x;
-    if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
-    if (blk >= a.items) return;  // block-uniform
-    const int seg = blk % a.nseg;
-    const int n = blk / a.nseg;
-    const int p0 = seg * a.RB;
-    const int rbe = min(a.RB, a.H - p0);
-    const int nx = rbe + 4;      // x rows p0-2 .. p0+rbe+1
-    const int n1 = rbe + 2;      // intermediate rows p0-1 .. p0+rbe
-    const int nsteps = nx + 2;   // output row p0 + o completes at step o + 6
-    const int q0 = wr * SW;
-    const int HW = a.H * a.W;
-
-    // ---- A: x DMA, 4 instructions per wave: lane l of instruction i -> float4 e = 64 (4 wr + i) + l
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
-    const int W4 = a.Wp >> 2;
-    uint32_t vi[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int e = 64 * (4 * wr + i) + lane;
-        const int c = e / W4, q = 4 * (e - c * W4);
-        vi[i] = (isA && q < a.W) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
-    }
-    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
-    auto load_row = [&](int sl, int jn) __attribute__((always_inline)) {
-        const int h = p0 - 2 + jn;
-        const bool hok = jn < nx && h >= 0 && h < a.H;
-        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
-        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(4 * wr) * 1024u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            rows_dma16<true>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
-    };
-
-    // ---- A: split lanes: column sc = lane of the strip, both channel octets; halo lanes < 32
-    const int hside = lane >> 4, hch = lane & 15;
-    const int hq = hside ? q0 + SW : q0 - 1;
-    const bool h_ok = lane < 2 * CC && hq >= 0 && hq < a.W;
-    const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
-    const int rdx0 = (q0 + lane) * 4;
-    const int rdx_h = hch * (a.Wp * 4) + (h_ok ? hq : 0) * 4;
-    int aoff[NG][KS], yoff[NG][KS];
-    {
-        const int p = lane & 15, g = lane >> 4;
-#pragma unroll
-        for (int grp = 0; grp < NG; ++grp) {
-            const int qc = q0 + 16 * grp + p;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int sh = ks == 0 ? (g >> 1) : 2;
-                const bool zero = ks == 1 && g >= 2;
-                aoff[grp][ks] = zero ? zero_off : xa<CC>(16 * grp + p + sh, g & 1);
-                yoff[grp][ks] = zero ? yzero : yoct<CC>(qc + sh, g & 1);
-            }
-        }
-    }
-    const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * CC * HW, CC * HW * 4);
-
-    float scale1 = 1.0f, scale2 = 1.0f;
-    bool fin1 = true, fin2 = true;
-    bf16x8 bw[NF];  // A: conv 1's fragments (transposed form), B: conv 2's
-    float ek1[E ? 4 : 1], ek0[E ? 4 : 1];   // A: epilogue 1 folded: t = act1(acc * ek1[c] + ek0[c]), c = 4 (lane >> 4) + e
-    float ek2s = 1.0f, ek2b = 0.0f;         // B: channel lane & 15: v = acc * ek2s + ek2b
-    floatx4 acc[3][NG];
-#pragma unroll
-    for (int sl = 0; sl < 3; ++sl)
-#pragma unroll
-        for (int grp = 0; grp < NG; ++grp) acc[sl][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    // 3 tap rows x 2 k-steps x 3 planes x 4 groups of MFMAs on one split row into slots SL of S
-    auto mfmas = [&](auto S_, auto TR_, const unsigned char* pb, int plstride) __attribute__((always_inline)) {
-        constexpr int S = decltype(S_)::value;
-        constexpr bool TR = decltype(TR_)::value;
-        constexpr int SL[3] = {(S + 1) % 3, S, (S + 2) % 3};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            bf16x8 af[3][NG];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                for (int grp = 0; grp < NG; ++grp)
-                    af[pl][grp] = __builtin_bit_cast(
-                        bf16x8, *reinterpret_cast<const uint4*>(pb + pl * plstride + (TR ? aoff[grp][ks] : yoff[grp][ks])));
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {
-                const bf16x8 b = bw[rr * KS + ks];
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int grp = 0; grp < NG; ++grp)
-                        acc[SL[rr]][grp] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], acc[SL[rr]][grp], 0, 0, 0)
-                                              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, acc[SL[rr]][grp], 0, 0, 0);
-            }
-        }
-    };
-
-    // A: epilogue 1 of intermediate row i from slot D (values split straight into ring slot YW)
-    auto epi1 = [&](auto D_, auto YW_, int i) __attribute__((always_inline)) {
-        constexpr int D = decltype(D_)::value, YW = decltype(YW_)::value;
-        const int r1 = p0 - 1 + i;
-        const bool irow = i >= 0 && i < n1 && r1 >= 0 && r1 < a.H;
-        const int p = lane & 15, g = lane >> 4;
-        unsigned char* yw = yr + YW * yslot;
-#pragma unroll
-        for (int grp = 0; grp < NG; ++grp) {
-            const int q = q0 + 16 * grp + p;  // lane: pixel q, channels 4 g .. 4 g + 3
-            const bool ok = irow && q < a.W;
-            uint32_t b4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float t;
-                if constexpr (E == 0)
-                    t = acc[D][grp][e] * scale1 + 0.0f;
-                else
-                    t = epi_act(acc[D][grp][e] * ek1[e] + ek0[e], a.act1);
-                b4[e] = ok ? __float_as_uint(t) : 0u;
-            }
-            uint16_t h[4], m[4], l[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) split1(b4[e], h[e], m[e], l[e]);
-            const int wo = yoct<CC>(q + 1, g >> 1) + 8 * (g & 1);
-            *reinterpret_cast<uint2*>(yw + wo) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-            *reinterpret_cast<uint2*>(yw + a.YPL + wo) =
-                make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
-            *reinterpret_cast<uint2*>(yw + 2 * a.YPL + wo) =
-                make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
-            acc[D][grp] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-    };
-
-    // B: epilogue 2 of output row o from slot D: whole 128-byte lines per store (the DPP
-    // exchange of conv_pair's epi2 on group pairs (0, 1) and (2, 3))
-    auto epi2 = [&](auto D_, int o) __attribute__((always_inline)) {
-        constexpr int D = decltype(D_)::value;
-        const bool orow = o >= 0 && o < rbe;
-        const int g = lane >> 4;
-        const bool hi8 = (lane & 8) != 0;
-#pragma unroll
-        for (int gp = 0; gp < NG / 2; ++gp) {
-            floatx4 v0, v1;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float u0 = acc[D][2 * gp][e] * ek2s + ek2b, u1 = acc[D][2 * gp + 1][e] * ek2s + ek2b;
-                if constexpr (E != 0) {
-                    u0 = epi_act(u0, a.act2);
-                    u1 = epi_act(u1, a.act2);
-                }
-                v0[e] = u0;
-                v1[e] = u1;
-            }
-            floatx4 sa, sb;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v1[e]), 0x128, 0xf, 0xf, false));
-                const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v0[e]), 0x128, 0xf, 0xf, false));
-                sa[e] = hi8 ? r1 : v0[e];
-                sb[e] = hi8 ? v1[e] : r0;
-            }
-            const int q = q0 + 32 * gp + (hi8 ? 16 : 0) + 4 * g;
-            const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
-            const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
-            const bool ok = orow && q < a.W;
-            rows_store<true>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
-            rows_store<true>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
-            acc[D][2 * gp] = floatx4{0.f, 0.f, 0.f, 0.f};
-            acc[D][2 * gp + 1] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-    };
-
-    auto step = [&](auto S_, int j) __attribute__((always_inline)) {
-        constexpr int S6 = decltype(S_)::value;
-        constexpr int S = S6 % 3;
-        if (isA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x row j (own DMAs)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (isA) {
-            load_row((S6 + 1) & 1, j + 1);  // row j + 1 into the slot of row j - 1
-            const unsigned char* rw = raw + (S6 & 1) * rawslot;
-            uint32_t bx[2][8], hx;
-#pragma unroll
-            for (int so = 0; so < 2; ++so)
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    bx[so][e] = *reinterpret_cast<const uint32_t*>(rw + (8 * so + e) * (a.Wp * 4) + rdx0);
-            hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
-            // the deferred epilogue 1: intermediate row j - 3, completed at step j - 1 (slot D of
-            // S6 - 1), into ring slot (j - 3) & 1
-            epi1(std::integral_constant<int, ((S6 + 5) % 3 + 2) % 3>{}, std::integral_constant<int, (S6 + 1) & 1>{},
-                 j - 3);
-#pragma unroll
-            for (int so = 0; so < 2; ++so) {
-                uint4 hi, mid, lo;
-                split3<kPairPK>(bx[so], hi, mid, lo);
-                const int wa = xa<CC>(lane + 1, so);
-                *reinterpret_cast<uint4*>(slab + wa) = hi;
-                *reinterpret_cast<uint4*>(slab + PL + wa) = mid;
-                *reinterpret_cast<uint4*>(slab + 2 * PL + wa) = lo;
-            }
-            if (lane < 2 * CC) {
-                uint16_t h16, m16, l16;
-                split1(h_ok ? hx : 0u, h16, m16, l16);
-                *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
-                *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
-                *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
-            }
-            mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab, PL);
-        } else {
-            // conv 2 one step behind conv_pair's: intermediate row j - 4 from ring slot j & 1,
-            // the rotation of step j - 1, output row j - 6 completes
-            constexpr int SB = (S6 + 5) % 3;
-            if (j >= 4) mfmas(std::integral_constant<int, SB>{}, std::false_type{}, yr + (S6 & 1) * yslot, a.YPL);
-            epi2(std::integral_constant<int, (SB + 2) % 3>{}, j - 6);
-        }
-    };
-
-    // ---- prologue: x row 0 (A), both weights quantized + packed (scratch: the intermediate
-    // planes, zeroed after)
-    if (isA) load_row(0, 0);
-    {
-        unsigned* red = reinterpret_cast<unsigned*>(yr);
-        unsigned* thr = red + 16;
-        scale1 = wq_prologue(a.q1, thr, red, nw, fin1);
-        if (isA) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, 1, KS, f * 64 + lane, scale1, fin1, thr));
-        }
-        __syncthreads();
-        scale2 = wq_prologue(a.q2, thr, red, nw, fin2);
-        if (!isA) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, 1, KS, f * 64 + lane, scale2, fin2, thr));
-        }
-        if constexpr (E != 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int c = 4 * (lane >> 4) + e;
-                const float s = a.ps1 ? a.ps1[c] : 1.0f;
-                ek1[e] = scale1 * s;
-                ek0[e] = (a.b1 ? a.b1[c] : 0.0f) * s + (a.pb1 ? a.pb1[c] : 0.0f);
-            }
-            const int k = lane & 15;
-            const float s2 = a.ps2 ? a.ps2[k] : 1.0f;
-            ek2s = scale2 * s2;
-            ek2b = (a.b2 ? a.b2[k] : 0.0f) * s2 + (a.pb2 ? a.pb2[k] : 0.0f);
-        } else {
-            ek2s = scale2;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw[f]));
-        if constexpr (E != 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(ek1[e]), "+v"(ek0[e]));
-        }
-        asm volatile("" : "+v"(ek2s), "+v"(ek2b));
-        __syncthreads();
-        for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
-            reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
-        if (isA && lane < 3) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
-    }
-    for (int j = 0; j < nsteps; j += 6) {
-        step(std::integral_constant<int, 0>{}, j);
-        step(std::integral_constant<int, 1>{}, j + 1);
-        step(std::integral_constant<int, 2>{}, j + 2);
-        if (j + 3 >= nsteps) break;
-        step(std::integral_constant<int, 3>{}, j + 3);
-        step(std::integral_constant<int, 4>{}, j + 4);
-        step(std::integral_constant<int, 5>{}, j + 5);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // ------------------------------------------------------------------ planning --
 struct PairPlan {
@@ -1185,7 +759,6 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
                                 hipStream_t s) {
     const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
     const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
-    constexpr bool kStg = PD == 2 && NTS == 3;  // the stagger is instantiated for the default ring / store mode
 #ifdef PO2Q_PAIR_STAMPS
     if (plain && getenv("PO2Q_STAMPS")) {
         PairArgs as = a;
@@ -1218,30 +791,26 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
             if (res) {  // residual == x, read from the ring (checked by the caller)
                 if constexpr (PD >= 6) {
                     if (a.act1 == 1 && a.act2 == 1)
-                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 2, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 2, 0, 1>), grid, block8, pp.lds, s, x, y, a);
                     else
-                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1, 0, 1>), grid, block8, pp.lds, s, x, y, a);
                     return hipGetLastError();
                 }
                 return hipErrorInvalidValue;
             }
             if (plain)
-                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
             else
-                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1, 0, 0, 1>), grid, block8, pp.lds, s, x, y, a);
+                hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1, 0, 1>), grid, block8, pp.lds, s, x, y, a);
             return hipGetLastError();
         }
     }
-    if (kStg && plain && a.stg)
-        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
-    else if (plain)
+    if (plain)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 0>), grid, block, pp.lds, s, x, y, a);
     else if (res && a.act1 == 1 && a.act2 == 1)  // the BasicBlock form (resnet.py:55-71): ReLU / ReLU
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 2>), grid, block, pp.lds, s, x, y, a);
     else if (res)
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, true, 1>), grid, block, pp.lds, s, x, y, a);
-    else if (kStg && a.stg)
-        hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1, kStg ? 1 : 0>), grid, block, pp.lds, s, x, y, a);
     else
         hipLaunchKernelGGL((conv_pair<CC, PD, NTS, false, 1>), grid, block, pp.lds, s, x, y, a);
     return hipGetLastError();
@@ -1255,7 +824,7 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
         const dim3 grid((unsigned)pp.blocks), block(64 * pp.waves);
 #define PO2Q_PD(v) \
         if (dbg == v && pp.C == 16 && pp.pd == 2 && pp.nts == 3 && !res) { \
-            hipLaunchKernelGGL((conv_pair<16, 2, 3, false, 0, 0, v>), grid, block, pp.lds, s, x, y, a); \
+            hipLaunchKernelGGL((conv_pair<16, 2, 3, false, 0, v>), grid, block, pp.lds, s, x, y, a); \
             return hipGetLastError(); \
         }
         PO2Q_PD(1) PO2Q_PD(2) PO2Q_PD(3) PO2Q_PD(4) PO2Q_PD(8) PO2Q_PD(12) PO2Q_PD(16) PO2Q_PD(19)
@@ -1283,34 +852,18 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 // ------------------------------------------------------------------ C ABI --
 namespace {
 
-// variant knob: PO2Q_PAIR_VARIANT = halves * 1000 + prio * 100 + pd * 10 + nts (halves 1: C = 16
-// stores 64-byte half lines; prio 1: waves 4.. at issue
-// priority 1; pd 2 / 3 x ring slots; nts bit 0: non-temporal stores, bit 1 (pd 2 only):
-// non-temporal x loads); default 23: non-temporal
-// loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32 (bs = 256,
-// profiles/r02_pair_nt.log)
-void pair_variant(int& pd, int& nts, int& prio, int& halves, int& stg, int64_t C) {
+// variant knob: PO2Q_PAIR_VARIANT = prio * 100 + pd * 10 + nts (prio 1: waves 4.. at issue priority
+// 1; pd 2 / 3 x ring slots; nts bit 0: non-temporal stores, bit 1 (pd 2 only): non-temporal x loads);
+// default 23: non-temporal loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32
+// (bs = 256, profiles/r02_pair_nt.log)
+void pair_variant(int& pd, int& nts, int& prio, int64_t C) {
     pd = 2;
     nts = 3;
     // priority 1 for waves 4..: 0.494 vs 0.504 / 0.500 ms at C = 16 (both store modes), mixed at
     // C = 32 (profiles/r02_pair_prio.log)
     prio = C == 16 ? 1 : 0;
-    halves = 0;
-    stg = 0;
-    // C = 32 stores 64-byte half lines per wave (16 columns): non-temporal, the halves of a line
-    // from neighbouring waves reach HBM as two partial writes (1.35x the output bytes,
-    // r03_pmc_pair32_v7.json).  PO2Q_PAIR_C32_TS=1: temporal stores, merged in L2 (1.00x).
-    if (C == 32) {
-        const char* ts = getenv("PO2Q_PAIR_C32_TS");
-        if (ts && ts[0] == '1') nts = 2;
-    }
     if (const char* e = getenv("PO2Q_PAIR_VARIANT")) {
-        int v = atoi(e);
-        stg = v >= 20000 ? 2 : (v >= 10000 ? 1 : 0);  // + 10000: the stagger kernel (STG) where no residual is
-                                                      // added; + 20000: the role-split kernel (conv_pair_ab)
-        v %= 10000;
-        halves = v >= 1000 ? 1 : 0;  // + 1000: accepted, no effect (half-line stores were dropped in round 3)
-        v %= 1000;
+        const int v = atoi(e) % 1000;
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
         if (((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) ||
@@ -1370,8 +923,8 @@ int po2q_qconv2d_pair_supported(int64_t N, int64_t C, int64_t H, int64_t W, int 
         if (e && e[0] == '0') return 0;
     }
     po2q::PairPlan pp;
-    int pd, nts, prio, halves, stg;
-    pair_variant(pd, nts, prio, halves, stg, C);
+    int pd, nts, prio;
+    pair_variant(pd, nts, prio, C);
     return pair_args_ok(N, C, H, W, bits, fsr, mode, 0, 0) &&
                    po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, true, pd, nts)
                ? 1
@@ -1402,8 +955,8 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         return PO2Q_OK;
     }
     po2q::PairPlan pp;
-    int pd, nts, prio, halves, stg;
-    pair_variant(pd, nts, prio, halves, stg, C);
+    int pd, nts, prio;
+    pair_variant(pd, nts, prio, C);
     if (residual && C == 16 && !getenv("PO2Q_PAIR_VARIANT")) {
         // the BasicBlock form re-reads x as the residual five steps after its row DMA: with
         // temporal x loads that read hits L2, with non-temporal ones it goes back to memory.
@@ -1432,8 +985,6 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.ps2 = post_scale2; a.pb2 = post_shift2; a.act2 = act2;
     a.res = residual;
     a.prio = prio;
-    a.halves = halves;
-    a.stg = stg;
     a.stamps = nullptr;
     // The memory-wave kernel with a PD-slot x ring: the default at C = 16 (PD 5; 6 for the identity
     // residual read from the ring): 0.4286 vs 0.4385 ms for the plain pair 16 @224 bs 256, 4
@@ -1456,34 +1007,6 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
                 return PO2Q_ERR_UNSUPPORTED;
             }
         }
-    }
-    if (stg == 2 && C == 16 && !residual && W <= 4 * po2q::kABSW) {
-        // role-split kernel: 2 x ceil(W / 64) waves, the pair plan's row segments
-        po2q::PairABArgs b;
-        b.N = (int)N; b.H = (int)H; b.W = (int)W;
-        b.NR = (int)((W + po2q::kABSW - 1) / po2q::kABSW);
-        b.Wp = po2q::kABSW * b.NR;
-        b.YPL = (b.Wp + 3) * 32;
-        b.RB = pp.RB; b.nseg = pp.nseg; b.items = (int)(N * pp.nseg);
-        b.remap = (pp.blocks % 8 == 0) ? 1 : 0;
-        b.q1 = a.q1; b.q2 = a.q2;
-        b.b1 = bias1; b.b2 = bias2; b.ps1 = post_scale1; b.pb1 = post_shift1; b.ps2 = post_scale2; b.pb2 = post_shift2;
-        b.act1 = act1; b.act2 = act2;
-        const size_t lds = (size_t)2 * 16 * b.Wp * 4 + (size_t)2 * 3 * b.YPL + (size_t)b.NR * 3 * po2q::kABPlane;
-        const dim3 grid((unsigned)pp.blocks), block((unsigned)(128 * b.NR));
-        const bool plain = !bias1 && !bias2 && !post_scale1 && !post_shift1 && !post_scale2 && !post_shift2 &&
-                           act1 == 0 && act2 == 0;
-        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-        if (plain)
-            hipLaunchKernelGGL((po2q::conv_pair_ab<0>), grid, block, lds, st, x, y, b);
-        else
-            hipLaunchKernelGGL((po2q::conv_pair_ab<1>), grid, block, lds, st, x, y, b);
-        const hipError_t e2 = hipGetLastError();
-        if (e2 != hipSuccess) {
-            po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e2));
-            return PO2Q_ERR_HIP;
-        }
-        return PO2Q_OK;
     }
     const hipError_t e = po2q::launch_pair(pp, a, x, y, residual != nullptr, reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) {

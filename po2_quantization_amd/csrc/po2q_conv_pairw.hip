@@ -80,10 +80,12 @@ struct PairWArgs {
 // PD: x ring slots (2 or 3); NTS bit 0: non-temporal stores, bit 1: non-temporal x loads.
 // E: 0 = plain chain (y = scale * acc), 1 = general epilogues, 2 = the BasicBlock form (ReLU after both
 // BNs, the conv scale and bias folded into the BN affine at staging).
-template <int PD, int NTS, bool RES, int E>
+// DBG (diagnostic builds only, -DPO2Q_PAIRW_DIAG, PO2Q_PAIR_W32_DBG; timing only, outputs are wrong):
+// bit 1 no MFMAs, 2 no x DMAs, 4 no stores, 8 no epilogue / split vector work, 16 no per-step barrier.
+template <int PD, int NTS, bool RES, int E, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x, float* __restrict__ y,
                                                      PairWArgs a) {
-    static_assert(PD == 2 || PD == 3, "raw ring slots");
+    static_assert(PD >= 2 && PD <= 5, "raw ring slots");
     constexpr int CC = kPWC, SW = kPWSW, WC = SW + 2, PL = kPWPL, YPL = kPWYPL, RPB = kPWRPB;
     constexpr int NG = SW / 16, NT = CC / 16, KS = 3, NF = 3 * KS * NT;
     constexpr int yslot = 3 * YPL;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
 
     float scale = 1.0f;  // this wave's conv: scale1 (B) or scale2 (A)
     bool fin = true;
-    bf16x8 bw[NF];
+    bf16x8 bw[NF] = {};
     float bk[E ? NT * 4 : 1], es[E ? NT * 4 : 1], eb[E ? NT * 4 : 1];  // B: ch 16 nt + 4 (lane >> 4) + e; A: e = 0
     floatx4 acc[3][NG][NT];
 #pragma unroll
@@ -250,9 +252,31 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
         constexpr int D = (S + 2) % 3;          // the accumulator slot that completes
         constexpr int YW = (S6 + 1) & 1;        // ring slot written: intermediate row j - 3
         const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
-        rows_wait<VMW_B>();  // this wave's part of x row j has landed
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + everyone's reads of the slots refilled
-        load_x((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
+        if constexpr ((DBG & 32) != 0) {  // probe: two-row DMAs every other step, waited whole
+            if constexpr (S6 % 2 == 0) rows_wait<0>();
+        } else {
+            rows_wait<VMW_B>();  // this wave's part of x row j has landed
+        }
+        if constexpr ((DBG & 16) == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + everyone's reads of the slots refilled
+        if constexpr ((DBG & 32) != 0) {
+            // probe (timing only): rows j + 2, j + 3 of every channel as ONE run of 2 x W floats per channel
+            // (896 bytes at W = 112) instead of two 448-byte runs a step apart
+            if constexpr (S6 % 2 == 0) {
+                const int h = p0 + j;
+                const bool hok = h + 1 < a.H;
+                const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+                const uint32_t base = raw_lds + (uint32_t)((S6 / 2 % 2) * kPWRaw) + (uint32_t)(4 * sw) * 1024u;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int e = 64 * (8 * sw + i) + lane;  // float4 e of the [32][2 W / 4] pair
+                    const int c = e / 56, q = 4 * (e - c * 56);
+                    const uint32_t vo = (hok && c < CC) ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u + roff : 0x7fffffffu;
+                    rows_dma16<(NTS & 2) != 0>(rs, vo, 0u, base + (uint32_t)(i & 3) * 1024u);
+                }
+            }
+        } else if constexpr ((DBG & 2) == 0) {
+            load_x((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
+        }
         uint32_t bx[2][8], hx;
         {
             const unsigned char* rw = raw + RS * kPWRaw;
@@ -264,7 +288,7 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
             }
             hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
         }
-        {  // epilogue 1: affine / activation, zeros outside the image (conv 2's padding), exact split
+        if constexpr ((DBG & 8) == 0) {  // epilogue 1: affine / activation, zeros outside the image (conv 2's padding), exact split
             const int i1 = j - 3;
             const int r1 = p0 - 1 + i1;
             const bool irow = i1 >= 0 && i1 < n1 && r1 >= 0 && r1 < a.H;
@@ -301,7 +325,7 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
                 }
             }
         }
-        {  // the exact split of x row j into the strip's planes
+        if constexpr ((DBG & 8) == 0) {  // the exact split of x row j into the strip's planes
             uint4 hi, mid, lo;
             split3<false>(bx[0], hi, mid, lo);
             *reinterpret_cast<uint4*>(slab + wa0) = hi;
@@ -317,7 +341,7 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
             *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
             *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
         }
-        mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab);
+        if constexpr ((DBG & 1) == 0) mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab);
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp)
 #pragma unroll
@@ -335,9 +359,9 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
         constexpr int YR = S6 & 1;              // ring slot read: intermediate row j - 4
         const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
         if constexpr (RES) rows_wait<VMW_A>();  // the residual of output row j - 6 has landed
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + B's epilogue-1 writes
+        if constexpr ((DBG & 16) == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + B's epilogue-1 writes
         if constexpr (RES) load_res((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
-        mfmas(std::integral_constant<int, S>{}, std::false_type{}, yr + YR * yslot);
+        if constexpr ((DBG & 1) == 0) mfmas(std::integral_constant<int, S>{}, std::false_type{}, yr + YR * yslot);
         const int o = j - 6;
         const bool orow = o >= 0 && o < rbe;
         const unsigned char* rres_row = resr + RS * kPWRes;
@@ -380,8 +404,18 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
                                                                    0x128, 0xf, 0x3, false));
             }
             const uint32_t ca = (uint32_t)(16 * nt) + (uint32_t)(lane & 7), cb = ca + 8u;
-            rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
-            rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+            if constexpr ((DBG & 32) != 0) {  // probe: both rows of a pair stored back to back, every other step
+                if constexpr (S6 % 2 == 1) {
+                    const uint32_t ro2 = rowoff >= (uint32_t)a.W ? rowoff - (uint32_t)a.W : rowoff;
+                    rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + ro2) * 4u : 0x7fffffffu, sa);
+                    rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+                    rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + ro2) * 4u : 0x7fffffffu, sb);
+                    rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+                }
+            } else if constexpr ((DBG & 4) == 0) {
+                rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+                rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+            }
         }
     };
 
@@ -406,14 +440,14 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
         unsigned* thr = red + 16;
         bool fin1, fin2;
         const float scale1 = wq_prologue(a.q1, thr, red, 2 * kPWWaves, fin1);
-        if (!roleA) {
+        if (!roleA && (DBG & 128) == 0) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
                 bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr));
         }
         __syncthreads();  // red / thr reads of conv 1 done
         const float scale2 = wq_prologue(a.q2, thr, red, 2 * kPWWaves, fin2);
-        if (roleA) {
+        if (roleA && (DBG & 128) == 0) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
                 bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
@@ -463,6 +497,7 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
         // step 0's barrier publishes the zeros
     }
     (void)fin;
+    if constexpr ((DBG & 64) != 0) return;  // probe: launch + weight staging only
     if (roleA) {
         for (int j = 0; j < nsteps; j += 6) {
             stepA(std::integral_constant<int, 0>{}, j);
@@ -498,6 +533,19 @@ template <int PD, int NTS>
 hipError_t launch_pairw_t(int blocks, size_t lds, const PairWArgs& a, const float* x, float* y, bool res, hipStream_t s) {
     const bool plain = !res && !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
     const dim3 grid((unsigned)blocks), block(64 * 2 * kPWWaves);
+#ifdef PO2Q_PAIRW_DIAG
+    if (const char* dv = getenv("PO2Q_PAIR_W32_DBG")) {
+        const int dbg = atoi(dv);
+#define PO2Q_PWD(v) \
+        if (dbg == v && plain && NTS == 3) { \
+            hipLaunchKernelGGL((conv_pairw<PD, NTS, false, 0, v>), grid, block, lds, s, x, y, a); \
+            return hipGetLastError(); \
+        }
+        PO2Q_PWD(9) PO2Q_PWD(11) PO2Q_PWD(13) PO2Q_PWD(15) PO2Q_PWD(25) PO2Q_PWD(29) PO2Q_PWD(27)
+        PO2Q_PWD(31) PO2Q_PWD(64) PO2Q_PWD(192) PO2Q_PWD(128)
+#undef PO2Q_PWD
+    }
+#endif
     if (plain) {
         hipLaunchKernelGGL((conv_pairw<PD, NTS, false, 0>), grid, block, lds, s, x, y, a);
         return hipGetLastError();
@@ -538,7 +586,7 @@ hipError_t pairw_launch(const float* x, const float* w1, const float* w2, float*
     int pd = pairw_knob();
     const bool plain = !res && !bias1 && !bias2 && !post_scale1 && !post_shift1 && !post_scale2 && !post_shift2 &&
                        act1 == 0 && act2 == 0;
-    if (pd != 3 || !plain) pd = 2;  // the residual slots leave room for 2 x slots only
+    if (pd < 2 || pd > 5 || !plain) pd = 2;  // deeper rings for the plain form only (LDS with the residual slots)
     // non-temporal x loads and y stores, except with a residual: the residual re-reads x a few steps
     // after its row's DMA, which temporal loads leave in L2 (conv_pair's variant 21 at C = 16)
     int nts = res ? 1 : 3;
@@ -568,7 +616,7 @@ hipError_t pairw_launch(const float* x, const float* w1, const float* w2, float*
     if (pd == d && nts == t) return launch_pairw_t<d, t>(blocks, lds, a, x, y, res, s);
     PO2Q_PW(2, 3)
 #ifndef PO2Q_PAIRW_ISA
-    PO2Q_PW(3, 3) PO2Q_PW(2, 1)
+    PO2Q_PW(3, 3) PO2Q_PW(4, 3) PO2Q_PW(5, 3) PO2Q_PW(2, 1)
 #endif
 #undef PO2Q_PW
     return hipErrorInvalidValue;

@@ -53,7 +53,7 @@ SHAPES = [(2, 20, 32, 16), (1, 9, 224, 16), (3, 37, 68, 16), (2, 1, 36, 16), (1,
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
-@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123", "1123", "10123", "10023", "20023"])
+@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123"])
 def test_pair_chain_vs_torch(shape, variant, monkeypatch):
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", variant)
     N, H, W, C = shape
@@ -174,36 +174,6 @@ def test_pair_block_vs_oracle(C, W):
         y = _lib.qconv2d_pair(x, w1, w2, 4, mode, bias1=b1, act1="relu", act2="relu", residual=x, **e)
         ref = oracle_block(x, w1, w2, mode, e, "relu", "relu", x, bias1=b1)
         assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL, (mode, normwise_err(y.cpu().numpy(), ref))
-
-
-@pytest.mark.parametrize("C,W", [(16, 224), (16, 136), (32, 112)])
-def test_pair_stagger_bitwise_equal(C, W, monkeypatch):
-    """The stagger kernel (PO2Q_PAIR_VARIANT + 10000: waves 4.. run the conv-2 epilogue one step
-    late) moves work, not arithmetic: its output equals the default kernel's bit for bit."""
-    x, w1, w2, e = make(2, 21, W, 17, True, C)
-    for kw in ({}, dict(act1="relu", act2="relu", **e)):
-        monkeypatch.setenv("PO2Q_PAIR_VARIANT", "123")
-        ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
-        monkeypatch.setenv("PO2Q_PAIR_VARIANT", "10123")
-        y = _lib.qconv2d_pair(x, w1, w2, 4, "po2", **kw)
-        assert torch.equal(y, ref)
-
-
-@pytest.mark.parametrize("W", [224, 192, 136, 64, 8])
-def test_pair_role_split_kernel(W, monkeypatch):
-    """The role-split kernel (PO2Q_PAIR_VARIANT + 20000, conv_pair_ab: conv-1 waves and conv-2
-    waves paired on each SIMD) equals conv_pair on the plain chain up to fp32 summation order
-    (conv_pair pairs the s2 tap of two planes in one k-step, conv_pair_ab keeps one k-step per
-    plane) and meets the bar with BN + activation epilogues (folded affine)."""
-    x, w1, w2, e = make(2, 23, W, 29 + W, True, 16)
-    monkeypatch.setenv("PO2Q_PAIR_VARIANT", "23")
-    ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
-    monkeypatch.setenv("PO2Q_PAIR_VARIANT", "20023")
-    y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
-    assert nerr(y, ref) <= 1e-6, nerr(y, ref)
-    y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", act1="relu", act2="silu", **e)
-    ref = torch_chain(x, w1, w2, e, "relu", "silu", None, "po2+")
-    assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
 
 
 @pytest.mark.parametrize("pd", [3, 4, 5, 6])
