@@ -602,21 +602,20 @@ __global__ __launch_bounds__(512, 1) void conv_pair(const float* __restrict__ x,
     {
         unsigned* red = reinterpret_cast<unsigned*>(yr);
         unsigned* thr = red + 16;
+        uint4* fr = reinterpret_cast<uint4*>(yr + 4096);  // conv 1's fragments (and conv 2's for C = 16)
+        static_assert(4096 + (WL2 ? 1 : 2) * NF * 64 * 16 <= 2 * yslot, "fragment scratch");
         scale1 = wq_prologue(a.q1, thr, red, nw + MW, fin1);
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-            bw1[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr,
-                                                             CC == 16));
-        __syncthreads();  // red / thr reads of conv 1 done
+        wq_pack_rows_lds<CC>(a.q1, CC, CC, NT, KS, scale1, fin1, thr, fr, NF, CC == 16);
         scale2 = wq_prologue(a.q2, thr, red, nw + MW, fin2);
         if constexpr (WL2) {
-            for (int e = tid; e < NF * 64; e += blockDim.x) wl2[e] = wq_frag_rows(a.q2, CC, CC, CC, NT, KS, e, scale2, fin2, thr);
+            wq_pack_rows_lds<CC>(a.q2, CC, CC, NT, KS, scale2, fin2, thr, wl2, NF);
         } else {
+            wq_pack_rows_lds<CC>(a.q2, CC, CC, NT, KS, scale2, fin2, thr, fr + NF * 64, NF, CC == 16);
 #pragma unroll
-            for (int f = 0; f < NF; ++f)
-                bw2[WL2 ? 0 : f] = __builtin_bit_cast(
-                    bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr, CC == 16));
+            for (int f = 0; f < NF; ++f) bw2[WL2 ? 0 : f] = __builtin_bit_cast(bf16x8, fr[NF * 64 + f * 64 + lane]);
         }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) bw1[f] = __builtin_bit_cast(bf16x8, fr[f * 64 + lane]);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             if constexpr (E != 0) {

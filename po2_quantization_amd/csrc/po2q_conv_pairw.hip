@@ -438,19 +438,17 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
     {
         unsigned* red = reinterpret_cast<unsigned*>(yr);
         unsigned* thr = red + 16;
+        uint4* fr = reinterpret_cast<uint4*>(yr + 4096);  // 2 x NF fragments (36 KB of the 50 KB planes)
+        static_assert(4096 + 2 * NF * 64 * 16 <= 2 * yslot, "fragment scratch");
         bool fin1, fin2;
         const float scale1 = wq_prologue(a.q1, thr, red, 2 * kPWWaves, fin1);
-        if (!roleA && (DBG & 128) == 0) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q1, CC, CC, CC, NT, KS, f * 64 + lane, scale1, fin1, thr));
-        }
-        __syncthreads();  // red / thr reads of conv 1 done
+        if constexpr ((DBG & 128) == 0) wq_pack_rows_lds<CC>(a.q1, CC, CC, NT, KS, scale1, fin1, thr, fr, NF);
         const float scale2 = wq_prologue(a.q2, thr, red, 2 * kPWWaves, fin2);
-        if (roleA && (DBG & 128) == 0) {
+        if constexpr ((DBG & 128) == 0) {
+            wq_pack_rows_lds<CC>(a.q2, CC, CC, NT, KS, scale2, fin2, thr, fr + NF * 64, NF);
+            const uint4* frw = fr + (roleA ? NF * 64 : 0);
 #pragma unroll
-            for (int f = 0; f < NF; ++f)
-                bw[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q2, CC, CC, CC, NT, KS, f * 64 + lane, scale2, fin2, thr));
+            for (int f = 0; f < NF; ++f) bw[f] = __builtin_bit_cast(bf16x8, frw[f * 64 + lane]);
         }
         scale = roleA ? scale2 : scale1;
         fin = roleA ? fin2 : fin1;
@@ -567,7 +565,7 @@ hipError_t launch_pairw_t(int blocks, size_t lds, const PairWArgs& a, const floa
 // non-temporal x loads and y stores)
 int pairw_knob() {
     const char* e = getenv("PO2Q_PAIR_W32");
-    if (!e) return 0;  // measured slower than conv_pair<32> (0.419 vs 0.356 ms, profiles/r06_pairw_ab.jsonl): off
+    if (!e) return 2;  // PD 2: 0.305 vs 0.319 ms plain, 0.328 vs 0.351 block (profiles/r06_wpack_ab.jsonl)
     return atoi(e);
 }
 

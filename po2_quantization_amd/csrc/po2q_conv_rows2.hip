@@ -322,7 +322,7 @@ __global__ __launch_bounds__(SEG2 ? 512 : 448, SEG2 ? 1 : 2) void conv_rows2(con
         unsigned* thr = red + 16;
         scale = wq_prologue(a.q, thr, red, nw, fin);
         __syncthreads();  // every wave's scratch reads done before wl (disjoint) -- and thr stays
-        for (int e = tid; e < NF * 64; e += blockDim.x) wl[e] = wq_frag_rows(a.q, CC, K, CC, NT, KS, e, scale, fin, thr);
+        wq_pack_rows_lds<CC>(a.q, K, CC, NT, KS, scale, fin, thr, wl, NF);
         if constexpr (DS) {
             __syncthreads();  // thr / red reads of the 3x3 weight done
             scaled = wq_prologue(a.qd, thr, red, nw, find);

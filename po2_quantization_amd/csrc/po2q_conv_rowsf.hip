@@ -352,9 +352,7 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
         unsigned* thr = red + 16;
         if constexpr (FP) {
             scale = wq_prologue(a.q, thr, red, nw, fin);
-            if constexpr (!(V & 1))
-                for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x)
-                    wl[e] = wq_frag_rows(a.q, CC, CC, CC, NT, KS, e, scale, fin, thr);
+            if constexpr (!(V & 1)) wq_pack_rows_lds<CC>(a.q, CC, CC, NT, KS, scale, fin, thr, wl, 3 * KS * NT);
         } else {
             for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x) wl[e] = wpk[e];
             scale = *scale_p;

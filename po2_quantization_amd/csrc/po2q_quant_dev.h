@@ -170,6 +170,41 @@ __device__ __forceinline__ uint4 wq_frag_rows(const WQuant& q, int C, int K, int
     return make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
 }
 
+// Cooperative form of wq_frag_rows for the whole tensor: ONE coalesced pass over w, every weight
+// quantized + packed once per block (not once per lane that needs it, whose 1152-byte-strided
+// gathers made the per-lane form cost ~0.085 ms per stage-2 pair launch: profiles/r06_pairw_ablation),
+// its bf16 code written into the row-layout fragments in LDS.  fr: nfr * 64 uint4, zero-filled
+// here (k >= K, the CC = 16 halves no tap fills).  Same fragments as wq_frag_rows (C: the tensor's
+// input channels, a compile-time constant so the index split is a multiply).  Ends with a barrier.
+template <int C>
+__device__ __forceinline__ void wq_pack_rows_lds(const WQuant& q, int K, int CC, int NT, int ksteps, float scale,
+                                                 bool fin, const unsigned* thr, uint4* fr, int nfr, bool dup = false) {
+    static_assert(C > 0, "channels");
+    const int tid = threadIdx.x, nthr = (int)blockDim.x;
+    for (int e = tid; e < nfr * 64; e += nthr) fr[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    uint16_t* h = reinterpret_cast<uint16_t*>(fr);
+    const int n = K * C * 9;
+    for (int i = tid; i < n; i += nthr) {
+        const int k = i / (C * 9), rem = i - k * (C * 9);
+        const int c = rem / 9, tap = rem - c * 9;
+        const int r = tap / 3, s = tap - r * 3;
+        const uint16_t v = pack_one(q.w[i], scale, fin, q.mode, q.lo, q.hi, thr);
+        int ks, grp;
+        if (CC == 16) {
+            ks = s == 2 ? 1 : 0;
+            grp = (s == 2 ? 0 : 2 * s) + (c >> 3);
+        } else {
+            ks = (c >> 5) * 3 + s;
+            grp = (c & 31) >> 3;
+        }
+        const int j = ((r * ksteps + ks) * NT + (k >> 4)) * 64 + (k & 15) + 16 * grp;
+        h[j * 8 + (c & 7)] = v;
+        if (CC == 16 && s == 2 && dup) h[(j + 32) * 8 + (c & 7)] = v;
+    }
+    __syncthreads();
+}
+
 // Stage the threshold row (LDS) and reduce the scale; returns the conv's multiplier
 // (max|w|, or 1 where the reference's Q(w) itself is packed).  thr: PO2Q_THR_COUNT LDS
 // words, red: nw LDS words.  Ends with the block's threshold row visible to every thread.
