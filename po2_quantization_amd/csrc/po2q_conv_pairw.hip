@@ -237,6 +237,15 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
                 }
     };
 
+    // a skipped row's step: only the slot that starts at step S (mfmas' zero accumulator) changes
+    auto zero_slot = [&](auto S_) __attribute__((always_inline)) {
+        constexpr int SR = decltype(S_)::value;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[(SR + 1) % 3][grp][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    };
+
     // B: conv 1's completed accumulator slot, held in VGPRs until the next step's epilogue 1
     floatx4 pend[NG][NT];
 #pragma unroll
@@ -341,7 +350,15 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
             *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
             *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
         }
-        if constexpr ((DBG & 1) == 0) mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab);
+        if constexpr ((DBG & 1) == 0) {
+            // x rows outside the image (the fill steps' padding rows, past the segment) are zeros: their
+            // MFMAs would add exact zeros, so the wave skips them (wave-uniform) and only starts slot SL[0]
+            const int h = p0 - 2 + j;
+            if (j < nx && h >= 0 && h < a.H)
+                mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab);
+            else
+                zero_slot(std::integral_constant<int, S>{});
+        }
 #pragma unroll
         for (int grp = 0; grp < NG; ++grp)
 #pragma unroll
@@ -361,7 +378,14 @@ __global__ __launch_bounds__(512, 1) void conv_pairw(const float* __restrict__ x
         if constexpr (RES) rows_wait<VMW_A>();  // the residual of output row j - 6 has landed
         if constexpr ((DBG & 16) == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // + B's epilogue-1 writes
         if constexpr (RES) load_res((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
-        if constexpr ((DBG & 1) == 0) mfmas(std::integral_constant<int, S>{}, std::false_type{}, yr + YR * yslot);
+        if constexpr ((DBG & 1) == 0) {
+            // intermediate rows outside the image / segment were written as zeros by epilogue 1: skipped
+            const int i2 = j - 4, r2 = p0 - 1 + i2;
+            if (i2 >= 0 && i2 < n1 && r2 >= 0 && r2 < a.H)
+                mfmas(std::integral_constant<int, S>{}, std::false_type{}, yr + YR * yslot);
+            else
+                zero_slot(std::integral_constant<int, S>{});
+        }
         const int o = j - 6;
         const bool orow = o >= 0 && o < rbe;
         const unsigned char* rres_row = resr + RS * kPWRes;
