@@ -55,19 +55,14 @@ constexpr size_t kChainLdsMax = 160 * 1024;
 // hits 64 distinct banks when a 16-pixel group is 16 consecutive pixels).  W8 (C = 64, W = 8: a
 // group is two 8-pixel row pieces 10 padded pixels apart): the octet XORed with a per-column
 // table instead (exhaustive search over every tap offset, tools-free: 3 bits per column).
-template <int C, bool W8 = false, bool S16 = false>
-__device__ __forceinline__ int ch_addr(int pp, int col, int oc, int oct = 0) {
+template <int C, bool W8 = false>
+__device__ __forceinline__ int ch_addr(int pp, int col, int oc) {
     if constexpr (C == 16) {
-        // S16 (PO2Q_CHAIN_VARIANT bit 1): the octet flipped with pixel bit 3, so pixels p and p + 8 of a
-        // 16-pixel group sit on different banks for the fragment reads (ds_read_b128) and the epilogue
-        // writes (ds_write_b64); [pixel][octet] (the default) puts them on the same banks (PMC: 34 % of
-        // the LDS cycles conflicted, profiles/r05_pmc_chain16.json; tools/lds_probe.hip: reads 81 vs 49
-        // cycles, writes 112 vs 61).  Measured slower in the kernel all the same, like the octet-major
-        // layout tried first ([octet][pixel]): MFMA phase 4,570 -> 7,258 cycles per layer, epilogue
-        // unchanged, config 2 813k -> 759k img/s (r05_ab_chain_bit3.jsonl, r05_chain_stamps_bit3.txt;
-        // octet-major: r05_ab_chain_octet_major.jsonl) -- the conflicts are not what bounds the chain,
-        // the per-step address work (pinned by the sched_barriers) is.  Off.  oct: unused
-        return S16 ? pp * 32 + 16 * (oc ^ ((pp >> 3) & 1)) : pp * 32 + 16 * oc;
+        // [pixel][octet]: pixels p and p + 8 of a group share banks (PMC: 34 % of the LDS cycles
+        // conflicted, profiles/r05_pmc_chain16.json), yet both swizzles tried (octet flipped with pixel
+        // bit 3; octet-major planes) were slower in the kernel: config 2 813k -> 759k img/s
+        // (r05_ab_chain_bit3.jsonl, r05_ab_chain_octet_major.jsonl)
+        return pp * 32 + 16 * oc;
     } else if constexpr (C == 32) {
         return pp * 64 + 16 * (oc ^ (((pp >> 2) & 1) << 1));
     } else if constexpr (W8) {
@@ -105,7 +100,6 @@ struct ChainArgs {
     int H, W, L;
     int PW, PL, ZO;
     int res0;             // 1: x itself is a later layer's residual: hold it
-    int prio;             // 1: the second wave of each SIMD (waves 4..7) issues at priority 1
     unsigned* stamps;     // PO2Q_CHAIN_STAMPS diagnostic builds only: per (block, wave) phase cycle sums
     ChainLayer layer[kChainMax];
 };
@@ -151,7 +145,7 @@ constexpr bool kChainPK = PO2Q_CHAIN_PK != 0;
 // DB (C = 32 / 64): two plane sets, layer l reads set l & 1 and writes set (l + 1) & 1, so the
 // barrier between a layer's MFMA phase and its epilogue goes: a wave's epilogue runs under the
 // other waves' MFMAs, one barrier per layer.
-template <int C, int MG, bool W8 = false, bool FULL = false, bool S16 = false, bool DB = false>
+template <int C, int MG, bool W8 = false, bool FULL = false, bool DB = false>
 __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __restrict__ x, float* __restrict__ y,
                                                                ChainArgs a) {
     constexpr int KS = C == 16 ? 2 : 3 * (C / 32);  // k-steps per tap row
@@ -169,7 +163,6 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
     const int n = blockIdx.x;
     const int nt = wave % NT, gsub = wave / NT;
     const int H = a.H, W = a.W, PW = a.PW, HW = H * W;
-    const int OCT = (H + 2) * PW * 16;  // S16 (C = 16): bytes per octet half-plane
     const int ngroups = (HW + 15) >> 4;
     const int p = lane & 15, g4 = lane >> 4;
     const int c0 = 16 * nt + 4 * g4;  // this lane's 4 output channels (transposed form)
@@ -193,7 +186,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             const float* src = xn + (int64_t)(8 * oc) * HW + (inb ? h * W + xc : 0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[i][e] = inb ? __float_as_uint(src[(int64_t)e * HW]) : 0u;
-            dst[i] = ok ? ch_addr<C, W8, S16>(rr * PW + pc, pc, oc, OCT) : -1;
+            dst[i] = ok ? ch_addr<C, W8>(rr * PW + pc, pc, oc) : -1;
         }
 #pragma unroll
         for (int i = 0; i < kChainItems; ++i) {
@@ -262,9 +255,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         constexpr int gi = st / (3 * KS), t = st % (3 * KS), r = t / KS, ks = t % KS;
         if constexpr (C == 16) {
             const int s = ks == 0 ? (g4 >> 1) : 2;
-            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C, W8, S16>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1, OCT);
+            return (ks == 1 && g4 >= 2) ? a.ZO : ch_addr<C, W8>(pp0[gi] + r * PW + s, px0[gi] + s, g4 & 1);
         } else {
-            return ch_addr<C, W8, S16>(pp0[gi] + r * PW + ks % 3, px0[gi] + ks % 3, (ks / 3) * 4 + g4);
+            return ch_addr<C, W8>(pp0[gi] + r * PW + ks % 3, px0[gi] + ks % 3, (ks / 3) * 4 + g4);
         }
     };
     constexpr int T = 3 * KS;    // MFMA steps (x 3 planes) per group
@@ -314,12 +307,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         // (s0 | s1) steps, or plus a per-lane offset (the two k-halves' tap rows / planes) for the
         // paired s2 steps.  The last pair's zero half reads the r2 lo unit again (finite: the split
         // clamps mid / lo) against zero weights, so it needs no zero slot.
-        // S16: the swizzle flips address bit 4 (the octet) with bit 8 (pixel bit 3) of the pixel's
-        // address within its plane; the plane offset is added after the flip
         constexpr int PXB = 32;
         const int OCB = 16;
-        (void)OCT;
-        int lb[MG], dsel[5], drow[5], dpl[5];
+        int lb[MG], dsel[5];
 #pragma unroll
         for (int gi = 0; gi < MG; ++gi) lb[gi] = (pp0[gi] + 2) * PXB + OCB * (g4 & 1);  // tap s = 2
 #pragma unroll
@@ -327,22 +317,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
             const int ua = 2 * u, ub = u == 4 ? 8 : 2 * u + 1;
             const int ra = ua / 3, pa = ua % 3, rb = ub / 3, pb = ub % 3;
             dsel[u] = g4 < 2 ? ra * PW * PXB + pa * a.PL : rb * PW * PXB + pb * a.PL;
-            drow[u] = g4 < 2 ? ra * PW * PXB : rb * PW * PXB;
-            dpl[u] = g4 < 2 ? pa * a.PL : pb * a.PL;
         }
         const int s01 = ((g4 >> 1) - 2) * PXB;  // tap (g4 >> 1) relative to the s = 2 base
-        auto flip = [](int b) __attribute__((always_inline)) { return b ^ ((b >> 4) & 16); };
         auto addr = [&](auto ST_) __attribute__((always_inline)) {
             constexpr int st = decltype(ST_)::value;
             constexpr int t = FULL ? st / MG : st % T1, gi = FULL ? st % MG : st / T1;  // FULL: k-step major
-            if constexpr (S16) {
-                if constexpr (t < 9) {
-                    constexpr int r = t / 3, pl = t % 3;
-                    return flip(lb[gi] + s01 + r * PW * PXB) + pl * a.PL;
-                } else {
-                    return flip(lb[gi] + drow[t - 9]) + dpl[t - 9];
-                }
-            } else if constexpr (t < 9) {
+            if constexpr (t < 9) {
                 constexpr int r = t / 3, pl = t % 3;
                 return lb[gi] + s01 + (r * PW * PXB + pl * a.PL);
             } else {
@@ -367,7 +347,6 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
         static_for<S1>(step);
     };
 
-    if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
     for (int l = 0; l < a.L; ++l) {
         const ChainLayer ly = a.layer[l];  // one batch of scalar loads for the whole descriptor
         const int rd = DB ? (l & 1) * 3 * a.PL : 0, wr = DB ? ((l + 1) & 1) * 3 * a.PL : 0;
@@ -482,7 +461,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain(const float* __re
                 } else {
                     // padded pixel (oy + 1, ox + 1) of output pixel f = (oy, ox): pp0 / px0 hold (oy, ox) of
                     // tap (0, 0), so no division by W here
-                    const int ad = ch_addr<C, W8, S16>(pp0[gi] + PW + 1, px0[gi] + 1, c0 >> 3, OCT) + 8 * ((c0 >> 2) & 1);
+                    const int ad = ch_addr<C, W8>(pp0[gi] + PW + 1, px0[gi] + 1, c0 >> 3) + 8 * ((c0 >> 2) & 1);
                     uint2 hi, mid, lo;
                     const uint32_t vb[4] = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                                             __float_as_uint(v[3])};
@@ -663,11 +642,6 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     a.PL = (int)chain_plane(C, H, W);
     a.ZO = a.PL - 16;
     a.res0 = used[0];
-    {  // PO2Q_CHAIN_PRIO=1: waves 4..7 at issue priority 1 (A/B knob; off: config 2 827.5k vs 826.7k
-       // img/s, 4 interleaved rounds, profiles/r05_ab_chain_prio.jsonl)
-        const char* pe = getenv("PO2Q_CHAIN_PRIO");
-        a.prio = (pe && pe[0] == '1') ? 1 : 0;
-    }
     for (int l = 0; l < n_layers; ++l) {
         ChainLayer& ly = a.layer[l];
         ly.wp = reinterpret_cast<const uint4*>(packed[l]);
@@ -679,8 +653,7 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
         ly.res_add = (res_from && res_from[l] >= 0) ? 1 : 0;
         ly.keep = used[l + 1];
     }
-    // PO2Q_CHAIN_VARIANT (A/B knob): bit 0 the checked form everywhere, bit 1 C = 16 planes
-    // swizzled, bit 3 one plane set.  Default: double-buffered planes for C = 32 / 64 (two sets
+    // PO2Q_CHAIN_VARIANT (test knob): bit 0 the checked form everywhere, bit 3 one plane set.  Default: double-buffered planes for C = 32 / 64 (two sets
     // fit): 0.0849 vs 0.0861 ms at 32 x 16^2 and 0.0782 vs 0.0795 at 64 x 8^2, 17 layers bs 256,
     // 5 of 5 interleaved rounds (profiles/r04_chain_ab_db.jsonl)
     const char* venv = getenv("PO2Q_CHAIN_VARIANT");
@@ -696,16 +669,11 @@ int po2q_qconv2d_chain_f32(const float* x, const float* const* w, const float* c
     auto launch = [&](const ChainArgs& a) -> bool {
 #define PO2Q_CH(c, m, w)                                                                               \
     if (C == c && mg <= m && w8 == w) {                                                                \
-        if (c == 16 && (variant & 2)) {                                                                \
+        if (c != 16 && db) {                                                                           \
             if (full && mg == m)                                                                       \
                 hipLaunchKernelGGL((conv_chain<c, m, w, true, true>), grid, block, lds, s, x, y, a);   \
             else                                                                                       \
                 hipLaunchKernelGGL((conv_chain<c, m, w, false, true>), grid, block, lds, s, x, y, a);  \
-        } else if (c != 16 && db) {                                                                    \
-            if (full && mg == m)                                                                       \
-                hipLaunchKernelGGL((conv_chain<c, m, w, true, false, true>), grid, block, lds, s, x, y, a); \
-            else                                                                                       \
-                hipLaunchKernelGGL((conv_chain<c, m, w, false, false, true>), grid, block, lds, s, x, y, a); \
         } else if (full && mg == m) {                                                                  \
             hipLaunchKernelGGL((conv_chain<c, m, w, true>), grid, block, lds, s, x, y, a);            \
         } else {                                                                                       \

@@ -837,11 +837,8 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
     PO2Q_PR(16, 5, 3) PO2Q_PR(32, 2, 3)
     return hipErrorInvalidValue;
 #endif
-    PO2Q_PR(16, 2, 0) PO2Q_PR(16, 3, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 3, 1)
-    PO2Q_PR(32, 2, 0) PO2Q_PR(32, 3, 0) PO2Q_PR(32, 2, 1) PO2Q_PR(32, 3, 1)
-    PO2Q_PR(16, 2, 2) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 2) PO2Q_PR(32, 2, 3)
-    PO2Q_PR(16, 3, 3) PO2Q_PR(16, 4, 3) PO2Q_PR(16, 5, 3) PO2Q_PR(16, 6, 3)
-    PO2Q_PR(32, 3, 3) PO2Q_PR(32, 4, 3) PO2Q_PR(32, 5, 3)
+    PO2Q_PR(16, 2, 0) PO2Q_PR(16, 2, 1) PO2Q_PR(16, 2, 3) PO2Q_PR(32, 2, 0) PO2Q_PR(32, 2, 3)
+    PO2Q_PR(16, 5, 3) PO2Q_PR(16, 6, 3)
 #undef PO2Q_PR
     return hipErrorInvalidValue;
 }
@@ -851,10 +848,10 @@ static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float
 // ------------------------------------------------------------------ C ABI --
 namespace {
 
-// variant knob: PO2Q_PAIR_VARIANT = prio * 100 + pd * 10 + nts (prio 1: waves 4.. at issue priority
-// 1; pd 2 / 3 x ring slots; nts bit 0: non-temporal stores, bit 1 (pd 2 only): non-temporal x loads);
-// default 23: non-temporal loads and stores, 0.485 vs 0.508 ms at C = 16 and 0.353 vs 0.364 at C = 32
-// (bs = 256, profiles/r02_pair_nt.log)
+// variant knob: PO2Q_PAIR_VARIANT = prio * 100 + 20 + nts (prio 1: waves 4.. at issue priority 1;
+// nts 3: non-temporal x loads and stores, 0: neither); default 23: 0.485 vs 0.508 ms at C = 16 and 0.353
+// vs 0.364 at C = 32 (bs = 256, profiles/r02_pair_nt.log).  The measured-off ring depth 3 and the
+// one-sided NT forms are gone, except 21 (non-temporal stores only), the C = 16 residual form's default.
 void pair_variant(int& pd, int& nts, int& prio, int64_t C) {
     pd = 2;
     nts = 3;
@@ -865,8 +862,7 @@ void pair_variant(int& pd, int& nts, int& prio, int64_t C) {
         const int v = atoi(e) % 1000;
         const int d = (v / 10) % 10, t = v % 10;
         prio = v >= 100 ? 1 : 0;  // + 100: priority 1 for waves 4.. (an explicit variant sets it)
-        if (((d == 2 || d == 3) && (t == 0 || t == 1 || (d == 2 && (t == 2 || t == 3)))) ||
-            (d >= 3 && d <= (C == 16 ? 6 : 5) && t == 3)) {
+        if (d == 2 && (t == 0 || t == 3 || (t == 1 && C == 16))) {
             pd = d;
             nts = t;
         }
@@ -987,8 +983,9 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     a.stamps = nullptr;
     // The memory-wave kernel with a PD-slot x ring: the default at C = 16 (PD 5; 6 for the identity
     // residual read from the ring): 0.4286 vs 0.4385 ms for the plain pair 16 @224 bs 256, 4
-    // interleaved rounds (profiles/r04_pair_mw_ab.jsonl); at C = 32 no gain (0.3401 vs 0.3394).
-    // PO2Q_PAIR_MW = PD (3..6) selects the ring depth, 0 the one-role kernel (A/B knob).
+    // interleaved rounds (profiles/r04_pair_mw_ab.jsonl); at C = 32 no gain (0.3401 vs 0.3394), and
+    // ring depths 3, 4 and 6 for the plain pair no different (r04_pair_mw_ab.jsonl): those variants are
+    // gone.  PO2Q_PAIR_MW=0 selects the one-role kernel (A/B and test knob).
     a.mw = 0;
     const char* mv = getenv("PO2Q_PAIR_MW");
     if (!mv && C == 16 && !getenv("PO2Q_PAIR_VARIANT")) mv = "5";
@@ -997,7 +994,7 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
         // with a residual: only the identity shortcut (residual == x), from a 6-slot ring
         const bool ring_res = residual != nullptr && residual == x && C == 16;
         const bool seven = W > 6 * (512 / C);  // the memory-wave kernel exists for 7 compute waves only
-        if (d >= 3 && d <= 6 && seven && (!residual || ring_res)) {
+        if (d == 5 && C == 16 && seven && (!residual || ring_res)) {
             a.mw = 1;
             pd = residual ? 6 : d;
             nts = 3;  // with the ring residual no x row is re-read from memory: non-temporal loads

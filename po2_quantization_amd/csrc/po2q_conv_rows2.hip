@@ -62,42 +62,33 @@ struct Rows2Args {
     const float* pbd;
 };
 
-// SEG2 (plan field PS = 2; C = 32, where one block's LDS leaves one block per CU): the block runs
-// TWO segments of the same image side by side, waves 0 .. nh-1 the first and nh .. 2nh-1 the
-// second, each half with its own x ring and planes and one copy of the weights for both: two waves
-// per SIMD instead of one.  Both halves run the same number of steps (the block-wide barrier), a
-// shorter last segment's extra steps load and store nothing.
-template <int CC, int PD, bool EPI, int NTS, int ND, bool DS = false, bool SEG2 = false>
-__global__ __launch_bounds__(SEG2 ? 512 : 448, SEG2 ? 1 : 2) void conv_rows2(const float* __restrict__ x,
-                                                                           const float* __restrict__ bias,
-                                                                           float* __restrict__ y, Rows2Args a) {
+template <int CC, int PD, bool EPI, int NTS, int ND, bool DS = false>
+__global__ __launch_bounds__(448, 2) void conv_rows2(const float* __restrict__ x, const float* __restrict__ bias,
+                                                     float* __restrict__ y, Rows2Args a) {
     static_assert(CC == 16 || CC == 32, "C = 16 or 32");
     static_assert(PD == 2 || PD == 4, "ring slots: 4 % PD == 0 keeps every index static");
     constexpr int K = 2 * CC, NT = K / 16, KS = kR2KS<CC>, NF = 3 * KS * NT;
     constexpr int PL = kR2Plane<CC>, OBASE = kR2EP * 2 * CC, ZOFF = (kR2EP + kR2OP) * 2 * CC;
-    constexpr int NR = SEG2 ? 2 : 1;                              // x rings (segments per block)
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nw = (int)(blockDim.x >> 6);
-    const int nh = nw / NR;                                       // waves per segment
-    const int half = SEG2 ? (wave >= nh ? 1 : 0) : 0;             // wave-uniform
-    const int wv = wave - half * nh;                              // wave within its segment
+    const int wv = wave;
     uint4* wl = reinterpret_cast<uint4*>(lds);                    // [NF][64] B fragments
-    unsigned char* raw = lds + NF * 1024 + half * PD * a.rawslot;  // PD slots [C][W] fp32
-    unsigned char* planes = lds + NF * 1024 + NR * PD * a.rawslot;  // every wave's planes
+    unsigned char* raw = lds + NF * 1024;                         // PD slots [C][W] fp32
+    unsigned char* planes = lds + NF * 1024 + PD * a.rawslot;     // every wave's planes
     unsigned char* slab = planes + wave * (3 * PL);               // this wave's planes
     uint4* wld = reinterpret_cast<uint4*>(planes + nw * (3 * PL));  // DS: [NT][64]
 
     int blk = blockIdx.x;
     if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
     if (blk >= a.items) return;  // block-uniform
-    const int seg = (blk % a.nseg) * NR + half;  // SEG2: a.nseg counts segment pairs
+    const int seg = blk % a.nseg;
     const int n = blk / a.nseg;
     const int p0 = seg * a.RB;
     const int rbe = max(0, min(a.RB, a.P - p0));
     const int nrows = 2 * rbe + 1;  // input rows 2 p0 - 1 .. 2 (p0 + rbe) - 1
-    const int nloop = SEG2 ? 2 * a.RB + 1 : nrows;  // steps run: the same in both halves
+    const int nloop = nrows;
     const int q0 = 16 * wv;         // first output column of the wave
 
     // ---- DMA: lane l of this wave's instruction i -> float4 e = 64 (ndma w + i) + l of the
@@ -374,10 +365,10 @@ __global__ __launch_bounds__(SEG2 ? 512 : 448, SEG2 ? 1 : 2) void conv_rows2(con
 }
 
 // ------------------------------------------------------------------ planning --
-static size_t rows2_lds(int C, int waves, int pd, int rawslot, int segs = 1) {  // segs 2: SEG2
+static size_t rows2_lds(int C, int waves, int pd, int rawslot) {
     const int nf = 3 * (C == 16 ? 2 : 3) * (2 * C / 16);
     const int plane = (kR2EP + kR2OP) * 2 * C + 32;
-    return (size_t)nf * 1024 + (size_t)segs * ((size_t)pd * rawslot + (size_t)waves * 3 * plane);
+    return (size_t)nf * 1024 + (size_t)pd * rawslot + (size_t)waves * 3 * plane;
 }
 
 void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vector<PlanCand>& out) {
@@ -436,45 +427,12 @@ void rows2_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 out.push_back({0.885 + 0.001 * (f - 1) + 0.002 * nts + 0.001 * (pd - 2), c});
             }
         }
-        // SEG2 (plan field PS = 2): two segments of an image per block sharing one weight copy,
-        // where the LDS leaves one block per CU (C = 32): an even segment count, one pair per block
-        if (per_cu == 1 && 2 * waves <= 8) {
-            ConvPlan c = q;
-            c.PS = 2;
-            c.nts = 0;
-            c.lds_bytes = rows2_lds(b.C, waves, pd, rawslot, 2);
-            const size_t dsb = (size_t)(2 * b.C / 16) * 1024;  // the shortcut's weight (s2ds)
-            if (c.lds_bytes + dsb <= 160 * 1024) {
-                int prev2 = -1;
-                for (int pairs : {1, 2}) {
-                    const int ns = std::min(2 * pairs, std::max(1, b.P / 4));
-                    if (ns < 2 || ns == prev2) break;
-                    prev2 = ns;
-                    c.TP = (b.P + ns - 1) / ns;
-                    c.tilesP = (b.P + c.TP - 1) / c.TP;  // segments (the last pair may hold an empty one)
-                    c.blocks = ((int64_t)b.N * ((c.tilesP + 1) / 2) + 7) / 8 * 8;
-                    out.push_back({0.889 + 0.001 * (pairs - 1), c});
-                }
-            }
-        }
     }
 }
 
 template <int CC, int PD, bool EPI, int NTS, int ND>
 static hipError_t launch_rows2_nd(const ConvPlan& p, const Rows2Args& a, const float* x, const float* bias, float* y,
                                   hipStream_t s) {
-    if constexpr (CC == 32 && PD == 2 && NTS == 0) {
-        if (p.PS == 2) {  // SEG2: two segments per block, twice the waves
-            const dim3 grid((unsigned)p.blocks), block(2 * 64 * (p.TQ / 16));
-            if (a.yds)
-                hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND, true, true>), grid, block,
-                                   p.lds_bytes + (size_t)(2 * CC / 16) * 1024, s, x, bias, y, a);
-            else
-                hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND, false, true>), grid, block, p.lds_bytes, s, x,
-                                   bias, y, a);
-            return hipGetLastError();
-        }
-    }
     if (p.PS != 0) return hipErrorInvalidValue;
     if (a.yds)
         hipLaunchKernelGGL((conv_rows2<CC, PD, EPI, NTS, ND, true>), dim3((unsigned)p.blocks), dim3(64 * (p.TQ / 16)),
@@ -507,7 +465,7 @@ hipError_t launch_conv_rows2(const ConvPlan& p, const float* x, const float* bia
     Rows2Args a;
     a.N = p.N; a.H = p.H; a.W = p.W; a.P = p.P; a.Q = p.Q;
     a.RB = p.TP;
-    a.nseg = p.PS == 2 ? (p.tilesP + 1) / 2 : p.tilesP;  // SEG2: segment pairs
+    a.nseg = p.tilesP;
     a.items = p.N * a.nseg;
     a.remap = (p.blocks % 8 == 0) ? 1 : 0;
     a.rawslot = p.dma_nck;
@@ -539,13 +497,8 @@ bool s2ds_plan(po2q::ConvPlan& p, int64_t N, int64_t C, int64_t H, int64_t W, in
     if (!po2q::plan_candidates(cands, N, C, H, W, 2 * C, 3, 3, 2, 2, 1, 1, 1, 1, 1, mode, bits, fsr, PO2Q_PREC_BF16X3))
         return false;
     const int want = C == 16 ? 4 : 2;
-    // PO2Q_S2DS_SEG2=1: the two-segment blocks (SEG2, plan field PS = 2) at C = 32.  Off by default:
-    // the bench step is the same with them (10.732 vs 10.742 ms, 3 rounds, profiles/r05_ab_s2ds_seg2.jsonl)
-    // -- one wave per SIMD was not what held the C = 32 transition back
-    const char* e2 = getenv("PO2Q_S2DS_SEG2");
-    const int want_ps = (C == 32 && e2 && e2[0] == '1') ? 2 : 0;
     int pick = -1;
-    auto score = [&](const po2q::ConvPlan& c) { return (c.pd == want ? 2 : 0) + (c.PS == want_ps ? 1 : 0); };
+    auto score = [&](const po2q::ConvPlan& c) { return c.pd == want ? 1 : 0; };
     for (int i = 0; i < (int)cands.size(); ++i) {
         const po2q::ConvPlan& c = cands[i];
         if (c.kind != po2q::KIND_BF16X3_ROWS || c.vrx != 5 || c.nts != 0) continue;

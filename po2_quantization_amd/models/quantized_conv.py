@@ -182,10 +182,9 @@ def can_fuse(*mods):
 # records which layers do that and at which shapes; later forwards at that shape pack them
 # up front.  False: every layer packs its own weight (A/B runs).
 BATCHED_PACKS = True
-# True: the batched packs run on a side stream, overlapping the stem.  Off: measured slower in the
-# graphed model lines (config 3 521k -> 493k img/s, config 5 13.77k -> 13.47k; the fork / join of
-# the second queue costs more than the ~30 us of packs it hides; profiles/r05_ab_side_packs.jsonl).
-SIDE_STREAM_PACKS = os.environ.get("PO2Q_SIDE_PACKS", "0") == "1"
+# The batched packs run inline on the forward's stream: a side stream overlapping the stem measured
+# slower in the graphed model lines (config 3 521k -> 493k img/s, config 5 13.77k -> 13.47k; the fork /
+# join of the second queue costs more than the ~30 us of packs it hides; profiles/r05_ab_side_packs.jsonl).
 # The active forward's _ForwardPacks, per thread: concurrent eval forwards (threads, DataParallel
 # replicas) each see only their own session.
 _tls = threading.local()
@@ -208,34 +207,12 @@ class _ForwardPacks:
         groups = {}
         for m, g, conf, plan in layers:
             groups.setdefault(conf, []).append((m, g, plan))
-        # The batched packs run on a side stream, concurrently with the model's stem and first layers
-        # (which read no packed weight); the first layer that reads a pack joins it (lookup), and the
-        # session end joins it when none did, so every fork is joined (a captured graph requires it).
-        cur = torch.cuda.current_stream(layers[0][0].weight.device) if layers else None
-        side = _side_stream(cur.device) if cur is not None else None
-        if side is not None:
-            side.wait_stream(cur)
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            for conf, items in groups.items():
-                bits, mode, prec = conf
-                ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g, _ in items], bits, mode, 1,
-                                     prec, plans=[pl for _, _, pl in items])
-                for (m, g, pl), w in zip(items, ws):
-                    self.ws[id(m)] = (g, m.weight, w, pl, conf)
-        self.ready = None
-        if side is not None:
-            self.ready = torch.cuda.Event()
-            self.ready.record(side)
-            self.stream = cur
-            if not torch.cuda.is_current_stream_capturing():
-                for hit in self.ws.values():  # made on the side stream, read on the forward's
-                    hit[2].record_stream(cur)
-
-    def join(self):
-        """Make the forward's stream wait for the batched packs (once)."""
-        if self.ready is not None:
-            self.stream.wait_event(self.ready)
-            self.ready = None
+        for conf, items in groups.items():
+            bits, mode, prec = conf
+            ws = _lib.pack_batch([(m.weight, g[0], g[1], g[2], g[3], g[4]) for m, g, _ in items], bits, mode, 1,
+                                 prec, plans=[pl for _, _, pl in items])
+            for (m, g, pl), w in zip(items, ws):
+                self.ws[id(m)] = (g, m.weight, w, pl, conf)
 
     def lookup(self, conv, g, weight):
         """The pack of `conv` when it was made for this geometry, this weight tensor and the layer's
@@ -245,21 +222,7 @@ class _ForwardPacks:
             return None
         if hit[4] != (conv.bits, NATIVE_MODES.get(conv.quantize_fn), conv.precision):
             return None
-        self.join()
         return hit
-
-
-_side_streams = {}
-
-
-def _side_stream(device):
-    """One side stream per device for the batched weight packs (SIDE_STREAM_PACKS; None: inline)."""
-    if not SIDE_STREAM_PACKS:
-        return None
-    s = _side_streams.get(device)
-    if s is None:
-        s = _side_streams[device] = torch.cuda.Stream(device)
-    return s
 
 
 # model -> {forward key: recorded layers}; weak, so a dropped model takes its records with it
@@ -287,8 +250,6 @@ def batched_packs(model, x):
         yield
     finally:
         _tls.packs = None
-        if sess.recording is None:
-            sess.join()
     if sess.recording is not None:
         rec[key] = sess.recording
 

@@ -135,28 +135,30 @@ def test_session_ignores_modules_of_other_models():
 
 
 @pytest.mark.parametrize("name,image", [("mobilenet", 32), ("mobilevit", 64)])
-def test_side_stream_packs_ordered_and_graph_capturable(name, image, monkeypatch):
-    """The batched packs on the side stream (SIDE_STREAM_PACKS): logits bit for bit those of inline
-    packs; an in-place weight update queued on the forward's stream just before the forward is seen
-    (the side stream waits for it); and the forward captures into a HIP graph whose replays match."""
+def test_batched_packs_see_weight_updates_and_graph_capture(name, image):
+    """The batched packs re-quantize every forward: an in-place weight update queued just before a
+    forward is seen (logits equal those of the per-layer packs); the forward captures into a HIP graph
+    whose replays match."""
     torch.manual_seed(5)
     m = get_model(name, 10, quantizer_dict["po2+"], 4, (image, image)).to(DEV).eval()
     x = torch.randn(8, 3, image, image, device=DEV)
-    monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", False)
     with torch.no_grad():
         m(x)
-        ref = m(x)
-    monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", True)
-    with torch.no_grad():
-        assert torch.equal(m(x), ref)
+        before = m(x)
         convs = [c for c in m.modules() if isinstance(c, qc.QuantizedConv2d)]
         for c in convs:
             c.weight.mul_(0.5)
         y = m(x)
-        monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", False)
-        ref2 = m(x)
-        monkeypatch.setattr(qc, "SIDE_STREAM_PACKS", True)
-        assert torch.equal(y, ref2)
+        qc.BATCHED_PACKS = False
+        try:
+            ref2 = m(x)  # every layer packs its own (updated) weight
+        finally:
+            qc.BATCHED_PACKS = True
+        # the per-layer path may pick other (fused-staging) plans: equal within the conv bar, and far
+        # from the logits of the weights before the update
+        err = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()  # noqa: E731
+        assert err(y, ref2) <= 1e-5 and err(before, ref2) > 1e-2
+        ref2 = y
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -53,7 +53,7 @@ SHAPES = [(2, 20, 32, 16), (1, 9, 224, 16), (3, 37, 68, 16), (2, 1, 36, 16), (1,
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
-@pytest.mark.parametrize("variant", ["20", "30", "21", "31", "22", "23", "123"])
+@pytest.mark.parametrize("variant", ["20", "23", "123"])
 def test_pair_chain_vs_torch(shape, variant, monkeypatch):
     monkeypatch.setenv("PO2Q_PAIR_VARIANT", variant)
     N, H, W, C = shape
@@ -176,9 +176,8 @@ def test_pair_block_vs_oracle(C, W):
         assert normwise_err(y.cpu().numpy(), ref) <= CONV_TOL, (mode, normwise_err(y.cpu().numpy(), ref))
 
 
-@pytest.mark.parametrize("pd", [3, 4, 5, 6])
-@pytest.mark.parametrize("shape", [(2, 23, 224, 16), (1, 224, 224, 16), (3, 9, 200, 16), (2, 30, 112, 32),
-                                   (1, 112, 112, 32), (2, 7, 100, 32)])
+@pytest.mark.parametrize("pd", [5])
+@pytest.mark.parametrize("shape", [(2, 23, 224, 16), (1, 224, 224, 16), (3, 9, 200, 16), (2, 31, 208, 16)])
 def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     """The memory-wave kernel (PO2Q_PAIR_MW = ring slots: an eighth wave issues every x DMA, the
     compute waves issue none) moves the loads, not the arithmetic: bit for bit the one-role kernel's
@@ -186,8 +185,6 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
     default is the memory wave itself), plain and with the general (BN + activation) epilogue; and
     within the bar of torch's fp32 chain on Q(w)."""
     N, H, W, C = shape
-    if C == 32 and pd > 5:
-        pytest.skip("C = 32: at most 5 ring slots fit the LDS")
     x, w1, w2, e = make(N, H, W, 41 + pd, True, C)
     forms = [{}, dict(act1="relu", act2="relu6", **e)]
     if C == 16:  # the identity residual read from the x ring (BasicBlock form and the general epilogue)

@@ -213,5 +213,8 @@ def test_lin_errors_and_autograd():
         _lib.quantize_lin(torch.randn(0, 4, 3, 3, device=DEV), 4, False)
     with pytest.raises(_lib.Po2qError, match="bits"):
         _lib.quantize_lin(torch.randn(2, 4, 3, 3, device=DEV), 0, False)
-    with pytest.raises(_lib.Po2qError, match="HIP device"):
-        _lib.quantize_lin(torch.randn(2, 4, 3, 3), 4, False)
+    # a CPU tensor takes the product's torch restatement of the reference ops (the CPU drop-in path):
+    # the same values as the HIP kernel
+    wc = torch.randn(2, 4, 3, 3)
+    for plus in (False, True):
+        assert torch.equal(_lib.quantize_lin(wc, 4, plus), _lib.quantize_lin(wc.to(DEV), 4, plus).cpu())
