@@ -584,13 +584,13 @@ hipError_t launch_pairw_t(int blocks, size_t lds, const PairWArgs& a, const floa
     return hipErrorInvalidValue;
 }
 
-// PO2Q_PAIR_W32: 0 turns the 4-wave kernel off (A/B runs: conv_pair<32> takes the shape), a number
-// 2 / 3 sets the plain form's ring depth; PO2Q_PAIR_W32_NTS the store / load policy (default 3:
-// non-temporal x loads and y stores)
+// PO2Q_PAIR_W32=0 turns the role-split kernel off (A/B and test knob: conv_pair<32> takes the shape);
+// on by default: 0.305 vs 0.319 ms plain, 0.328 vs 0.351 block, bench 25.2k vs 24.8k img/s
+// (profiles/r06_wpack_ab.jsonl).  PO2Q_PAIR_W32_NTS the store / load policy (default 3: non-temporal x
+// loads and y stores)
 int pairw_knob() {
     const char* e = getenv("PO2Q_PAIR_W32");
-    if (!e) return 2;  // PD 2: 0.305 vs 0.319 ms plain, 0.328 vs 0.351 block (profiles/r06_wpack_ab.jsonl)
-    return atoi(e);
+    return (e && e[0] == '0') ? 0 : 1;
 }
 
 }  // namespace
@@ -605,10 +605,8 @@ hipError_t pairw_launch(const float* x, const float* w1, const float* w2, float*
                         const float* post_scale1, const float* post_shift1, int act1, const float* post_scale2,
                         const float* post_shift2, const float* residual, int act2, hipStream_t s) {
     const bool res = residual != nullptr;
-    int pd = pairw_knob();
-    const bool plain = !res && !bias1 && !bias2 && !post_scale1 && !post_shift1 && !post_scale2 && !post_shift2 &&
-                       act1 == 0 && act2 == 0;
-    if (pd < 2 || pd > 5 || !plain) pd = 2;  // deeper rings for the plain form only (LDS with the residual slots)
+    // x ring depth 2: depths 3 - 5 (plain form) measured the same (profiles/r06_pairw_ablation.jsonl, pd2-5)
+    const int pd = 2;
     // non-temporal x loads and y stores, except with a residual: the residual re-reads x a few steps
     // after its row's DMA, which temporal loads leave in L2 (conv_pair's variant 21 at C = 16)
     int nts = res ? 1 : 3;
@@ -638,7 +636,7 @@ hipError_t pairw_launch(const float* x, const float* w1, const float* w2, float*
     if (pd == d && nts == t) return launch_pairw_t<d, t>(blocks, lds, a, x, y, res, s);
     PO2Q_PW(2, 3)
 #ifndef PO2Q_PAIRW_ISA
-    PO2Q_PW(3, 3) PO2Q_PW(4, 3) PO2Q_PW(5, 3) PO2Q_PW(2, 1)
+    PO2Q_PW(2, 1)
 #endif
 #undef PO2Q_PW
     return hipErrorInvalidValue;

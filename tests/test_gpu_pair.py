@@ -211,7 +211,7 @@ def test_pair_w32_bitwise_equal_7wave_kernel(shape, monkeypatch):
     whole-line stores; the default for C = 32 at 96 < W <= 128) runs the 7-wave conv_pair<32>'s
     arithmetic -- the same fragments, the same MFMA order per accumulator, the same epilogue expressions
     -- so its output is bit for bit the 7-wave kernel's (PO2Q_PAIR_W32=0) in the plain, general and
-    BasicBlock forms, at both ring depths of the plain form; ragged widths and 1-row images included."""
+    BasicBlock forms; ragged widths and 1-row images included."""
     N, H, W, C = shape
     x, w1, w2, e = make(N, H, W, 51 + W + H, True, C)
     g = torch.Generator().manual_seed(W)
@@ -221,10 +221,9 @@ def test_pair_w32_bitwise_equal_7wave_kernel(shape, monkeypatch):
     for kw in forms:
         monkeypatch.setenv("PO2Q_PAIR_W32", "0")
         ref = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", **kw)
-        for knob in (("2", "3") if not kw else ("2",)):
-            monkeypatch.setenv("PO2Q_PAIR_W32", knob)
-            y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", **kw)
-            assert torch.equal(y, ref), (shape, knob, sorted(kw), nerr(y, ref))
+        monkeypatch.setenv("PO2Q_PAIR_W32", "1")
+        y = _lib.qconv2d_pair(x, w1, w2, 4, "po2+", **kw)
+        assert torch.equal(y, ref), (shape, sorted(kw), nerr(y, ref))
     t = torch_chain(x, w1, w2, e, "relu", "relu", x, "po2+")
     monkeypatch.delenv("PO2Q_PAIR_W32", raising=False)
     assert nerr(_lib.qconv2d_pair(x, w1, w2, 4, "po2+", **forms[2]), t) <= CONV_TOL
