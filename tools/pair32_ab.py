@@ -16,7 +16,8 @@ from tools.tile_sweep import timeit  # noqa: E402
 
 
 def main():
-    N, C, H = int(os.environ.get("PAIR_N", "256")), 32, int(os.environ.get("PAIR_H", "112"))
+    C = int(os.environ.get("PAIR_C", "32"))
+    N, H = int(os.environ.get("PAIR_N", "256")), int(os.environ.get("PAIR_H", "224" if C == 16 else "112"))
     dev = torch.device("cuda:0")
     arms = [a for a in os.environ.get("PAIR_AB_ARMS", "PO2Q_PAIR_W32=0;PO2Q_PAIR_W32=2").split(";") if a]
     form = os.environ.get("PAIR_AB_FORM", "plain")
