@@ -135,6 +135,11 @@ for s in $STEPS; do
                  python3 tools/traffic.py gpurun_out/pmc_tpair --algorithmic 1644274688 --out gpurun_out/traffic.json >> gpurun_out/traffic.log 2>&1
                  run pmc_pair 600 bash tools/pmc.sh "--pair --shape 16,224,16,3,1,1" pair "conv_pair" all
                  python3 tools/pmc_summary.py gpurun_out/pmc_pair 355.3 > gpurun_out/pmc_pair_summary.txt 2>&1 ;;
+        pmc_pairw)  # the stage-2 role-split pair (conv_pairw): useful bf16 MFMA work 2 x 177.6 GFLOP
+                 run pmc_pairw 600 bash tools/pmc.sh "--pair --shape 32,112,32,3,1,1" pairw "conv_pairw" all
+                 python3 tools/pmc_summary.py gpurun_out/pmc_pairw 355.3 > gpurun_out/pmc_pairw_summary.txt 2>&1 ;;
+        profhead) run profhead 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profhead -o run \
+                  -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cifar --no-models ;;
         stamps) run stamps 600 python tools/stamps.py ;;
         pmcr1) run pmcr1 900 bash tools/pmc.sh "--shape 16,224,16,3,1,1" r1 "conv_bf16x3|conv_x3p" all ;;
         pmcr3) run pmcr3 900 bash tools/pmc.sh "--shape 64,56,64,3,1,1" r3 "conv_bf16x3|conv_x3p" all ;;

@@ -42,6 +42,7 @@ def main(d, mfma_gflop=None):
         simd_cycles = 1024 * v["GRBM_GUI_ACTIVE"] / 8  # GRBM_GUI_ACTIVE sums the 8 XCDs
         out["mfma_busy_frac"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles, 3)
         if mfma_gflop:
+            out["mfma_useful_gflop"] = mfma_gflop  # the argument the useful fraction is computed from
             out["mfma_useful_frac"] = round(mfma_gflop * 1e9 / 16384 * 16 / simd_cycles, 3)
     if "SQ_LDS_BANK_CONFLICT" in v and "SQ_LDS_IDX_ACTIVE" in v:
         out["lds_conflict_frac"] = round(v["SQ_LDS_BANK_CONFLICT"] / max(1.0, v["SQ_LDS_IDX_ACTIVE"]), 3)
