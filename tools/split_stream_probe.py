@@ -6,12 +6,16 @@ interleaved median ms per full-batch step for each split count and whether the l
 single-stream run bit for bit.
 
     python tools/split_stream_probe.py [splits=1,2,4] [rounds=3] [steps=20]
+    SPLIT_SEQ=1: the micro-batches one after another on one stream (chunk-major: a stage-3 or
+    stage-2 activation of a micro-batch fits the 256 MB MALL between consecutive layers)
 """
 import json
 import os
 import sys
 
 import torch
+
+SEQ = False
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -20,6 +24,8 @@ from po2_quantization_amd import _lib  # noqa: E402
 
 
 def main():
+    global SEQ
+    SEQ = os.environ.get("SPLIT_SEQ", "0") == "1"
     splits = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4").split(",")]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
@@ -42,6 +48,8 @@ def main():
         streams = [torch.cuda.Stream() for _ in parts]
 
         def step(chains=chains, parts=parts, streams=streams):
+            if SEQ:  # chunk-major on one stream: each micro-batch walks every layer before the next starts
+                return torch.cat([c.forward(p) for c, p in zip(chains, parts)])
             cur = torch.cuda.current_stream()
             outs = []
             for c, p, s in zip(chains, parts, streams):
