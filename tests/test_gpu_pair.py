@@ -93,7 +93,12 @@ def test_pair_equals_two_fused_calls(C, W):
 
 @pytest.mark.parametrize("C,H", [(16, 224), (32, 112)])
 def test_pair_full_size(C, H):
-    """BASELINE size (bs = 256 @224: stage 1, and stage 2 @112): against torch's fp32 chain."""
+    """BASELINE size (bs = 256 @224: stage 1, and stage 2 @112) at the bench's exact launch geometry:
+    against torch's fp32 chain on every image, and against the fp64 oracle (oracle/oracle.py qconv2d,
+    conv1 then conv2 on its output) on sampled images -- the first and last block of the grid, and
+    images whose blocks land on different XCDs of the remapped grid."""
+    from oracle import oracle as O
+
     torch.manual_seed(0)
     x = torch.relu(torch.randn(256, C, H, H, device=DEV))
     w1 = torch.randn(C, C, 3, 3, device=DEV) * (0.12 if C == 16 else 0.08)
@@ -101,6 +106,13 @@ def test_pair_full_size(C, H):
     y = _lib.qconv2d_pair(x, w1, w2, 4, "po2")
     ref = torch_chain(x, w1, w2, {}, "none", "none", None)
     assert nerr(y, ref) <= CONV_TOL, nerr(y, ref)
+    idx = [0, 37, 130, 255]
+    xs = x[idx].cpu().numpy()
+    h, _ = O.qconv2d(xs, w1.cpu().numpy(), None, 1, 1, 1, 1, 4, "po2")
+    o, _ = O.qconv2d(h.astype("float32"), w2.cpu().numpy(), None, 1, 1, 1, 1, 4, "po2")
+    ys = y[idx].cpu().numpy().astype("float64")
+    err = abs(ys - o).max() / abs(o).max()
+    assert err <= CONV_TOL, err
 
 
 def test_pair_rejects():

@@ -76,6 +76,15 @@ def test_s2ds_full_size(C, H):
     del ref
     refds = F.conv2d(x, _lib.quantize(wds, 4, "po2"), None, 2, 0)
     assert nerr(yds, refds) <= CONV_TOL, nerr(yds, refds)
+    # the bench's launch geometry against the fp64 oracle on sampled images (grid ends, other XCDs)
+    from oracle import oracle as O
+
+    idx = [0, 37, 130, 255]
+    xs = x[idx].cpu().numpy()
+    for out, wt, st, pad in ((y, w, 2, 1), (yds, wds, 2, 0)):
+        o, _ = O.qconv2d(xs, wt.cpu().numpy(), None, st, pad, 1, 1, 4, "po2")
+        err = abs(out[idx].cpu().numpy().astype("float64") - o).max() / abs(o).max()
+        assert err <= CONV_TOL, err
 
 
 def test_s2ds_rejects():
