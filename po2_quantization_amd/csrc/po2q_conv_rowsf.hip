@@ -352,7 +352,8 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
         unsigned* thr = red + 16;
         if constexpr (FP) {
             scale = wq_prologue(a.q, thr, red, nw, fin);
-            if constexpr (!(V & 1)) wq_pack_rows_lds<CC>(a.q, CC, CC, NT, KS, scale, fin, thr, wl, 3 * KS * NT);
+            // the block packs every fragment once into wl (V & 1 then copies its own into VGPRs)
+            wq_pack_rows_lds<CC>(a.q, CC, CC, NT, KS, scale, fin, thr, wl, 3 * KS * NT);
         } else {
             for (int e = tid; e < 3 * KS * NT * 64; e += blockDim.x) wl[e] = wpk[e];
             scale = *scale_p;
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(448, (CC == 32 && (V & 1)) ? 2 : 4) void conv_rowsf
 #pragma unroll
             for (int f = 0; f < 3 * KS * NT; ++f) {
                 if constexpr (FP)
-                    bwr[f] = __builtin_bit_cast(bf16x8, wq_frag_rows(a.q, CC, CC, CC, NT, KS, f * 64 + lane, scale, fin, thr));
+                    bwr[f] = __builtin_bit_cast(bf16x8, wl[f * 64 + lane]);
                 else
                     bwr[f] = __builtin_bit_cast(bf16x8, wpk[f * 64 + lane]);
             }

@@ -231,13 +231,18 @@ __global__ __launch_bounds__(LW ? kThreads + 64 : kThreads, C == 64 ? (TT ? 2 : 
         unsigned* thr = red + 16;
         bool fin;
         scale = wq_prologue(a.q, thr, red, 4, fin);
+        // one tap row's fragments at a time, packed by the whole block from coalesced weight reads
+        // into the (still unused) planes, then each wave takes its own (wq_pack_tap_row_lds)
+        uint4* fr = reinterpret_cast<uint4*>(planes);
+        static_assert(KSC * WN * 64 * 16 <= 2 * 3 * PL, "fragment scratch in the planes");
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < 3; ++r) {
+            wq_pack_tap_row_lds<C>(a.q, C, 32, WN, KSC, r, scale, fin, thr, fr);
 #pragma unroll
-            for (int ks = 0; ks < KSC; ++ks)
-                bw[r][ks] = __builtin_bit_cast(
-                    bf16x8, wq_frag_rows(a.q, C, C, 32, WN, KSC, ((r * KSC + ks) * WN + wn) * 64 + lane, scale, fin, thr));
-        __syncthreads();  // every threshold read done before the ring's DMAs
+            for (int ks = 0; ks < KSC; ++ks) bw[r][ks] = __builtin_bit_cast(bf16x8, fr[(ks * WN + wn) * 64 + lane]);
+            __syncthreads();  // every wave's reads of row r done before row r + 1 (or the splits) overwrite fr
+        }
+        // (the last barrier also orders every threshold read before the ring's DMAs)
     } else {
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -643,11 +648,14 @@ void rowsk_candidates(const ConvPlan& b, int mode, int bits, int fsr, std::vecto
                 const int64_t items = (int64_t)p.N * d.tilesP * d.tilesQ;
                 d.blocks = (items + 7) / 8 * 8;
                 out.push_back({0.9 + 0.001 * i + (pd == 2 ? 0.01 : 0.0) + (vrx == vrxs[0] ? 0.0 : 0.02), d});
-                // C = 64 direct stores with fused weight staging (one launch per layer)
+                // C = 64 direct stores with fused weight staging (one launch per layer): an autotune
+                // candidate, not the heuristic default -- every block re-packs the 36,864 weights, so
+                // even the cooperative staging leaves it at 0.298 ms against 0.164 ms + a ~7 us pack
+                // for the packed plan at bs 256 @56 (profiles/r06_plan_sweep_fp.jsonl)
                 if (b.C == 64 && vrx == 1) {
                     ConvPlan f = d;
                     f.fp = 1;
-                    out.push_back({0.899 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), f});
+                    out.push_back({0.95 + 0.001 * i + (pd == 2 ? 0.01 : 0.0), f});
                 }
                 // the default variants (C = 64 direct stores, C = 32 loader wave) also with
                 // non-temporal output stores (nts 1), non-temporal x loads (2) or both (3)

@@ -205,6 +205,36 @@ __device__ __forceinline__ void wq_pack_rows_lds(const WQuant& q, int K, int CC,
     __syncthreads();
 }
 
+// The same for tap row r only (kernels whose LDS scratch holds one tap row's fragments at a time):
+// fr gets fragments j = (ks * NT + nt) * 64 + lane of row r (wq_frag_rows index minus r's offset).
+template <int C>
+__device__ __forceinline__ void wq_pack_tap_row_lds(const WQuant& q, int K, int CC, int NT, int ksteps, int r,
+                                                    float scale, bool fin, const unsigned* thr, uint4* fr) {
+    static_assert(C > 0, "channels");
+    const int tid = threadIdx.x, nthr = (int)blockDim.x;
+    const int nfr = ksteps * NT;
+    for (int e = tid; e < nfr * 64; e += nthr) fr[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    uint16_t* h = reinterpret_cast<uint16_t*>(fr);
+    const int n = K * C * 3;  // (k, c, s) of tap row r
+    for (int m = tid; m < n; m += nthr) {
+        const int kc = m / 3, s = m - kc * 3;
+        const int k = kc / C, c = kc - k * C;
+        const uint16_t v = pack_one(q.w[kc * 9 + r * 3 + s], scale, fin, q.mode, q.lo, q.hi, thr);
+        int ks, grp;
+        if (CC == 16) {
+            ks = s == 2 ? 1 : 0;
+            grp = (s == 2 ? 0 : 2 * s) + (c >> 3);
+        } else {
+            ks = (c >> 5) * 3 + s;
+            grp = (c & 31) >> 3;
+        }
+        const int j = (ks * NT + (k >> 4)) * 64 + (k & 15) + 16 * grp;
+        h[j * 8 + (c & 7)] = v;
+    }
+    __syncthreads();
+}
+
 // Stage the threshold row (LDS) and reduce the scale; returns the conv's multiplier
 // (max|w|, or 1 where the reference's Q(w) itself is packed).  thr: PO2Q_THR_COUNT LDS
 // words, red: nw LDS words.  Ends with the block's threshold row visible to every thread.
