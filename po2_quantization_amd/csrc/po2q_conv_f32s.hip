@@ -338,13 +338,16 @@ void f32s_candidates(const ConvPlan& base, std::vector<PlanCand>& out) {
             c.cost = kb == 16 ? (items >= 65536 ? 0.5 : 1.0) : (items >= 65536 ? 1.0 : 0.5);
             out.push_back(c);
         }
-        {  // MI 1: conv_stem_f32, one output pixel x 8 channels per thread (the default)
+        {  // MI 1: conv_stem_f32, one output pixel x 8 channels per thread (the default up to ~1 M
+           // 4-pixel items; above, the 16-channel direct kernel: ResNet's 3 -> 16 @224 bs 256 0.331 vs
+           // 0.532 ms, MobileViT's 3 -> 16 s2 @256 bs 64 0.049 vs 0.052 the other way round,
+           // profiles/r06_stem_pkfma_ab.jsonl)
             ConvPlan q = p;
             q.MI = 1;
             q.blocks = ((int64_t)base.N * base.P * base.Q + 255) / 256;
             PlanCand c;
             c.plan = q;
-            c.cost = 0.0;
+            c.cost = items >= (1 << 20) ? 0.75 : 0.0;
             out.push_back(c);
         }
     }
