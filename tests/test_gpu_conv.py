@@ -602,3 +602,22 @@ def test_unquantized_kernels_every_plan_vs_oracle(shape):
     y = _lib.qconv2d_fused(xd, wd, bd, st, pad, 1, 1, 4, "none", post_scale=ps.to(DEV), post_shift=pb.to(DEV),
                            act="relu6").cpu().numpy()
     assert normwise_err(y, ref_e) <= CONV_TOL
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 56, 56), (64, 13, 44), (32, 20, 112), (16, 9, 224), (32, 7, 100)])
+def test_fused_staging_plans_equal_packed_plans(C, H, W):
+    """Every plan that quantizes + packs its weight inside the kernel (fp=1: the cooperative one-pass
+    staging of po2q_quant_dev.h wq_pack_rows_lds / wq_pack_tap_row_lds) gives bit for bit the output of
+    the same plan reading the separately packed weight (fp=0: pack_bf16x3_kernel), po2 and po2+."""
+    g = torch.Generator().manual_seed(C * H + W)
+    x = torch.randn(2, C, H, W, generator=g).to(DEV)
+    w = (torch.randn(C, C, 3, 3, generator=g) * 0.1).to(DEV)
+    for mode in ("po2", "po2+"):
+        ds = _lib.plans(2, C, H, W, C, 3, 3, 1, 1, mode=mode)
+        pairs = [(i, ds.index(d.replace(" fp=1", " fp=0"))) for i, d in enumerate(ds)
+                 if " fp=1" in d and d.replace(" fp=1", " fp=0") in ds]
+        assert pairs, (C, H, W, mode)
+        for i, j in pairs:
+            a = _lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, mode, plan=i)
+            b = _lib.qconv2d(x, w, None, 1, 1, 1, 1, 4, mode, plan=j)
+            assert torch.equal(a, b), (C, H, W, mode, ds[i])
