@@ -877,7 +877,7 @@ def main():
         pflops, pbytes = 2 * flops, 4.0 * (2 * B * 16 * Hs * Hs + 4 * 16 * 16 * 9)
         roof = roofline(pflops, pbytes, avg_ms)
         roof["traffic"] = traffic_of("pair16 %dx%d bs=%d" % (Hs, Hs, B))
-        roof.update({"kernel": "conv_pair<16> (po2q_qconv2d_pair_f32): layer1.0 conv1 -> conv2, 2 fused %s quantize+"
+        roof.update({"kernel": "conv_pair_rs16 (po2q_qconv2d_pair_f32, role-split pair): conv1 -> conv2, 2 fused %s quantize+"
                                "conv 3x3 16->16 @%dx%d bs=%d in one launch, intermediate on chip"
                                % (args.quantizer, Hs, Hs, B),
                      "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes": int(pbytes), "flops": int(pflops)})

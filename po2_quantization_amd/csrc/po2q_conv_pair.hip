@@ -720,6 +720,353 @@ struct PairPlan {
     size_t lds = 0;
 };
 
+// RS (C = 16, seven 32-column strips, no residual): the stage-1 pair with its two convs given to
+// different waves, as conv_pairw does at stage 2 -- waves 0-6 ("B") run conv 1 of strip w (their x DMAs,
+// the exact split, conv 1's MFMAs, the conv-1 epilogue one step later into the shared intermediate
+// ring), waves 7-13 ("A") run conv 2 of strip w - 7 on that ring and its epilogue with the stores.  A
+// wave's chain per step is one conv instead of both, and 14 waves give each SIMD 3-4 of them to
+// interleave.  Same fragments, same MFMA order per accumulator and the same epilogue expressions as
+// conv_pair<16>: the same bits.
+template <int PD, int NTS, int E>
+__global__ __launch_bounds__(896, 1) void conv_pair_rs16(const float* __restrict__ x, float* __restrict__ y,
+                                                         PairArgs a) {
+    static_assert(PD >= 2 && PD <= 4, "raw ring slots");  // the product instantiates PD 3
+    constexpr int CC = 16, SW = kQSW<16>, WC = SW + 2, PL = kQPlane<16>, KS = kQKS<16>;
+    constexpr int NG = SW / 16, NT = 1, NF = 3 * KS * NT, NWR = 7;
+    constexpr int YPL = (7 * SW + 3) * 2 * CC;
+    constexpr int yslot = 3 * YPL;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool roleA = wave >= NWR;  // wave-uniform: conv 2 (A) or conv 1 (B)
+    const int sw = roleA ? wave - NWR : wave;
+    const int RPB = a.Wp * 4;
+    const int rawslot = CC * RPB;
+    unsigned char* raw = lds;                                // PD x [C][Wp] fp32
+    unsigned char* yr = raw + PD * rawslot;                  // 2 x 3 planes (intermediate, split)
+    unsigned char* slab = yr + 2 * yslot + sw * (3 * PL);    // B: its strip's x planes
+    const int zero_off = WC * CC * 2;
+    constexpr int yzero = (7 * SW + 2) * (2 * CC);
+
+    int blk = blockIdx.x;
+    if (a.remap) blk = (blk & 7) * (int)(gridDim.x >> 3) + (blk >> 3);
+    if (blk >= a.items) return;  // block-uniform
+    const int seg = blk % a.nseg;
+    const int n = blk / a.nseg;
+    const int p0 = seg * a.RB;
+    const int rbe = min(a.RB, a.H - p0);
+    const int nx = rbe + 4;   // x rows p0-2 .. p0+rbe+1
+    const int n1 = rbe + 2;   // intermediate rows p0-1 .. p0+rbe
+    const int nsteps = nx + 2;  // output row p0 + o completes at step o + 6
+    const int q0 = sw * SW;
+    const int HW = a.H * a.W;
+
+    // ---- B: x DMA, conv_pair's mapping (lane l of instruction i -> float4 64(2 sw + i) + l of the row)
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(x + (int64_t)n * CC * HW, CC * HW * 4);
+    const int W4 = a.Wp >> 2;
+    uint32_t vi[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int e = 64 * (2 * sw + i) + lane;
+        const int c = e / W4, q = 4 * (e - c * W4);
+        vi[i] = q < a.W ? ((uint32_t)c * (uint32_t)HW + (uint32_t)q) * 4u : 0x7fffffffu;
+    }
+    const uint32_t raw_lds = (uint32_t)(uintptr_t)raw;
+    auto load_x = [&](int sl, int jn) __attribute__((always_inline)) {
+        const int h = p0 - 2 + jn;
+        const bool hok = jn < nx && h >= 0 && h < a.H;
+        const uint32_t roff = (uint32_t)(hok ? h : 0) * (uint32_t)a.W * 4u;
+        const uint32_t base = raw_lds + (uint32_t)(sl * rawslot) + (uint32_t)(2 * sw) * 1024u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            rows_dma16<(NTS & 2) != 0>(rs, (hok && vi[i] != 0x7fffffffu) ? vi[i] + roff : 0x7fffffffu, 0u, base + i * 1024u);
+    };
+    // ---- B: the split (conv_pair's split_x lanes: column sc, octet so; halo lanes)
+    const int sc = lane % SW, so = lane / SW;
+    const int wa_i = xa<CC>(sc + 1, so);
+    const int hl = lane % CC;
+    const int hside = hl / (CC / 2), hch = (CC / 2) * (lane >> 5) + hl % (CC / 2);
+    const int hq = hside ? q0 + SW : q0 - 1;
+    const bool h_ok = hq >= 0 && hq < a.W;
+    const int wa_h = xa<CC>(hside ? WC - 1 : 0, hch >> 3) + (hch & 7) * 2;
+    const int rdx0 = (so * 8) * RPB + (q0 + sc) * 4;
+    const int rdx_h = hch * RPB + (h_ok ? hq : 0) * 4;
+    // fragment offsets: conv_pair's (B: x planes, A: the shared intermediate planes)
+    int aoff[NG][KS], aoff2[NG];
+    {
+        const int p = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            const int qc = q0 + 16 * grp + p;
+            const int o = g & 1;
+            if (!roleA) {
+                aoff[grp][0] = xa<CC>(16 * grp + p + (g >> 1), o);
+                aoff[grp][1] = xa<CC>(16 * grp + p + 2, o) + (g >= 2 ? PL : 0);
+                aoff2[grp] = g >= 2 ? zero_off : xa<CC>(16 * grp + p + 2, o) + 2 * PL;
+            } else {
+                aoff[grp][0] = yoct<CC>(qc + (g >> 1), o);
+                aoff[grp][1] = yoct<CC>(qc + 2, o) + (g >= 2 ? YPL : 0);
+                aoff2[grp] = g >= 2 ? yzero : yoct<CC>(qc + 2, o) + 2 * YPL;
+            }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc(y + (int64_t)n * CC * HW, CC * HW * 4);
+    constexpr int VMW_B = 2 * (PD - 2);  // B: its DMAs of the PD - 2 rows issued after row j's
+
+    float scale = 1.0f;
+    bool fin = true;
+    bf16x8 bw[NF];
+    float bk[E ? NT * 4 : 1], es[E ? NT * 4 : 1], eb[E ? NT * 4 : 1];  // B: ch 4 (lane >> 4) + e; A: index 0
+    floatx4 acc[3][NG][NT];
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) acc[sl][grp][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // conv_pair's mfmas for one conv: per k-step the planes' fragments (k-step 1: the paired s2 ones),
+    // tap row 2 first, per accumulator k-step major, plane minor
+    auto mfmas = [&](auto S_, auto TR_, const unsigned char* pb) __attribute__((always_inline)) {
+        constexpr int SR = decltype(S_)::value;
+        constexpr bool TR = decltype(TR_)::value;
+        constexpr int SL[3] = {(SR + 1) % 3, SR, (SR + 2) % 3};
+        constexpr int PLS = TR ? PL : YPL;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int np = ks == 1 ? 2 : 3;
+            bf16x8 af[3][NG];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int grp = 0; grp < NG; ++grp) {
+                    if (pl >= np) continue;
+                    const int off = ks == 1 ? (pl == 0 ? aoff[grp][1] : aoff2[grp]) : pl * PLS + aoff[grp][0];
+                    af[pl][grp] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + off));
+                }
+#pragma unroll
+            for (int r3 = 0; r3 < 3; ++r3) {
+                const int rr = 2 - r3;
+                const bf16x8 b = bw[rr * KS + ks];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int grp = 0; grp < NG; ++grp) {
+                        if (pl >= np) continue;
+                        const floatx4 c = (rr == 0 && ks == 0 && pl == 0) ? floatx4{0.f, 0.f, 0.f, 0.f}
+                                                                         : acc[SL[rr]][grp][0];
+                        acc[SL[rr]][grp][0] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, af[pl][grp], c, 0, 0, 0)
+                                                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pl][grp], b, c, 0, 0, 0);
+                    }
+            }
+        }
+    };
+    auto zero_slot = [&](auto S_) __attribute__((always_inline)) {
+        constexpr int SR = decltype(S_)::value;
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) acc[(SR + 1) % 3][grp][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    };
+    floatx4 pend[NG];
+#pragma unroll
+    for (int grp = 0; grp < NG; ++grp) pend[grp] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- B, step j: epilogue 1 of intermediate row j - 3 (pend) into ring slot YW, the split of x row
+    // j, conv 1 on it (intermediate row j - 2 completes into pend)
+    auto stepB = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S6 = decltype(S_)::value;
+        constexpr int S = S6 % 3;
+        constexpr int D = (S + 2) % 3;
+        constexpr int YW = (S6 + 1) & 1;
+        const int RS = (6 % PD == 0) ? S6 % PD : j % PD;
+        rows_wait<VMW_B>();  // this wave's part of x row j has landed
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        load_x((6 % PD == 0) ? (S6 + PD - 1) % PD : (j - 1 + PD) % PD, j - 1 + PD);
+        uint32_t bx[8], hx;
+        {
+            const unsigned char* rw = raw + RS * rawslot;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bx[e] = *reinterpret_cast<const uint32_t*>(rw + rdx0 + e * RPB);
+            hx = *reinterpret_cast<const uint32_t*>(rw + rdx_h);
+        }
+        {
+            const int i1 = j - 3;
+            const int r1 = p0 - 1 + i1;
+            const bool irow = i1 >= 0 && i1 < n1 && r1 >= 0 && r1 < a.H;
+            const int p = lane & 15, g = lane >> 4;
+            unsigned char* yw = yr + YW * yslot;
+#pragma unroll
+            for (int grp = 0; grp < NG; ++grp) {
+                const int q = q0 + 16 * grp + p;
+                const bool okq = irow && q < a.W;
+                uint32_t b4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float t;
+                    if constexpr (E == 0) {
+                        t = pend[grp][e] * scale + 0.0f;
+                    } else if constexpr (E == 2) {
+                        t = pend[grp][e] * es[e] + eb[e];
+                        t = t < 0.0f ? 0.0f : t;
+                    } else {
+                        t = epi_act((pend[grp][e] * scale + bk[e]) * es[e] + eb[e], a.act1);
+                    }
+                    b4[e] = okq ? __float_as_uint(t) : 0u;
+                }
+                uint2 h2, m2, l2;
+                split4p<false>(b4, h2, m2, l2);
+                const int wo = yoct<CC>(q + 1, g >> 1) + 8 * (g & 1);
+                *reinterpret_cast<uint2*>(yw + wo) = h2;
+                *reinterpret_cast<uint2*>(yw + YPL + wo) = m2;
+                *reinterpret_cast<uint2*>(yw + 2 * YPL + wo) = l2;
+            }
+        }
+        {
+            uint4 hi, mid, lo;
+            split3<false>(bx, hi, mid, lo);
+            *reinterpret_cast<uint4*>(slab + wa_i) = hi;
+            *reinterpret_cast<uint4*>(slab + PL + wa_i) = mid;
+            *reinterpret_cast<uint4*>(slab + 2 * PL + wa_i) = lo;
+            uint16_t h16, m16, l16;
+            split1(h_ok ? hx : 0u, h16, m16, l16);
+            *reinterpret_cast<uint16_t*>(slab + wa_h) = h16;
+            *reinterpret_cast<uint16_t*>(slab + PL + wa_h) = m16;
+            *reinterpret_cast<uint16_t*>(slab + 2 * PL + wa_h) = l16;
+        }
+        {
+            const int h = p0 - 2 + j;  // rows outside the image are zeros: their MFMAs add exact zeros
+            if (j < nx && h >= 0 && h < a.H)
+                mfmas(std::integral_constant<int, S>{}, std::true_type{}, slab);
+            else
+                zero_slot(std::integral_constant<int, S>{});
+        }
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) pend[grp] = acc[D][grp][0];
+    };
+
+    // ---- A, step j: conv 2 on intermediate row j - 4 (ring slot YR), epilogue 2 of output row j - 6
+    // with conv_pair's whole-line DPP stores
+    auto stepA = [&](auto S_, int j) __attribute__((always_inline)) {
+        constexpr int S6 = decltype(S_)::value;
+        constexpr int S = S6 % 3;
+        constexpr int D = (S + 2) % 3;
+        constexpr int YR = S6 & 1;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        {
+            const int i2 = j - 4, r2 = p0 - 1 + i2;
+            if (i2 >= 0 && i2 < n1 && r2 >= 0 && r2 < a.H)
+                mfmas(std::integral_constant<int, S>{}, std::false_type{}, yr + YR * yslot);
+            else
+                zero_slot(std::integral_constant<int, S>{});
+        }
+        const int o = j - 6;
+        const bool orow = o >= 0 && o < rbe;
+        const int g = lane >> 4;
+        floatx4 vv[NG];
+#pragma unroll
+        for (int grp = 0; grp < NG; ++grp) {
+            floatx4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                v[e] = E == 0 ? acc[D][grp][0][e] * scale + 0.0f
+                       : E == 2 ? acc[D][grp][0][e] * es[0] + eb[0]
+                                : (acc[D][grp][0][e] * scale + bk[0]) * es[0] + eb[0];
+            if constexpr (E == 2) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] < 0.0f ? 0.0f : v[e];
+            } else if constexpr (E != 0) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], a.act2);
+            }
+            vv[grp] = v;
+        }
+        const bool hi8 = (lane & 8) != 0;
+        floatx4 sa, sb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sa[e] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(vv[0][e]), __float_as_int(vv[NG - 1][e]),
+                                                               0x128, 0xf, 0xc, false));
+            sb[e] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(vv[NG - 1][e]), __float_as_int(vv[0][e]),
+                                                               0x128, 0xf, 0x3, false));
+        }
+        const int q = q0 + (hi8 ? 16 : 0) + 4 * g;
+        const uint32_t rowoff = (uint32_t)(orow ? p0 + o : 0) * a.W + (uint32_t)q;
+        const uint32_t ca = (uint32_t)(lane & 7), cb = 8u + (uint32_t)(lane & 7);
+        const bool ok = orow && q < a.W;
+        rows_store<(NTS & 1) != 0>(ry, ok ? (ca * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sa);
+        rows_store<(NTS & 1) != 0>(ry, ok ? (cb * (uint32_t)HW + rowoff) * 4u : 0x7fffffffu, sb);
+    };
+
+    if (!roleA) {
+#pragma unroll
+        for (int r = 0; r < PD - 1; ++r) load_x(r, r);
+    }
+    {
+        unsigned* red = reinterpret_cast<unsigned*>(yr);
+        unsigned* thr = red + 16;
+        uint4* fr = reinterpret_cast<uint4*>(yr + 4096);
+        static_assert(4096 + 2 * NF * 64 * 16 <= 2 * yslot, "fragment scratch");
+        bool fin1, fin2;
+        const float scale1 = wq_prologue(a.q1, thr, red, 2 * NWR, fin1);
+        wq_pack_rows_lds<CC>(a.q1, CC, CC, NT, KS, scale1, fin1, thr, fr, NF, true);
+        const float scale2 = wq_prologue(a.q2, thr, red, 2 * NWR, fin2);
+        wq_pack_rows_lds<CC>(a.q2, CC, CC, NT, KS, scale2, fin2, thr, fr + NF * 64, NF, true);
+        const uint4* frw = fr + (roleA ? NF * 64 : 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) bw[f] = __builtin_bit_cast(bf16x8, frw[f * 64 + lane]);
+        scale = roleA ? scale2 : scale1;
+        fin = roleA ? fin2 : fin1;
+        if constexpr (E != 0) {
+            const float *b = roleA ? a.b2 : a.b1, *ps = roleA ? a.ps2 : a.ps1, *pb = roleA ? a.pb2 : a.pb1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = roleA ? (lane & 15) : 4 * (lane >> 4) + e;
+                bk[e] = b ? b[k] : 0.0f;
+                es[e] = ps ? ps[k] : 1.0f;
+                eb[e] = pb ? pb[k] : 0.0f;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (E != 0) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(bk[c]), "+v"(es[c]), "+v"(eb[c]));
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bw[f]));
+        if constexpr (E == 2) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                eb[c] = bk[c] * es[c] + eb[c];
+                es[c] = scale * es[c];
+            }
+        }
+        __syncthreads();  // scratch reads done: zero the intermediate planes and the x planes' zero slots
+        for (int e = tid; e < (2 * yslot) / 16; e += blockDim.x)
+            reinterpret_cast<uint4*>(yr)[e] = make_uint4(0u, 0u, 0u, 0u);
+        if (lane < 3 && !roleA) *reinterpret_cast<uint4*>(slab + lane * PL + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    (void)fin;
+    if (roleA) {
+        for (int j = 0; j < nsteps; j += 6) {
+            stepA(std::integral_constant<int, 0>{}, j);
+            stepA(std::integral_constant<int, 1>{}, j + 1);
+            stepA(std::integral_constant<int, 2>{}, j + 2);
+            if (j + 3 >= nsteps) break;
+            stepA(std::integral_constant<int, 3>{}, j + 3);
+            stepA(std::integral_constant<int, 4>{}, j + 4);
+            stepA(std::integral_constant<int, 5>{}, j + 5);
+        }
+    } else {
+        for (int j = 0; j < nsteps; j += 6) {
+            stepB(std::integral_constant<int, 0>{}, j);
+            stepB(std::integral_constant<int, 1>{}, j + 1);
+            stepB(std::integral_constant<int, 2>{}, j + 2);
+            if (j + 3 >= nsteps) break;
+            stepB(std::integral_constant<int, 3>{}, j + 3);
+            stepB(std::integral_constant<int, 4>{}, j + 4);
+            stepB(std::integral_constant<int, 5>{}, j + 5);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 static size_t pair_lds(int C, int waves, int pd, bool res, bool mw = false) {  // res: the compute waves' residual slots
     const int sw = 512 / C, wp = sw * waves;
     const int plane = (sw + 2) * 2 * C + 32;
@@ -815,8 +1162,23 @@ static hipError_t launch_pair_t(const PairPlan& pp, const PairArgs& a, const flo
     return hipGetLastError();
 }
 
+template <int PD>
+static hipError_t launch_pair_rs(const PairPlan& pp, const PairArgs& a, const float* x, float* y, hipStream_t s) {
+    const bool plain = !a.b1 && !a.b2 && !a.ps1 && !a.pb1 && !a.ps2 && !a.pb2 && a.act1 == 0 && a.act2 == 0;
+    const dim3 grid((unsigned)pp.blocks), block(64 * 14);
+    if (plain)
+        hipLaunchKernelGGL((conv_pair_rs16<PD, 3, 0>), grid, block, pp.lds, s, x, y, a);
+    else
+        hipLaunchKernelGGL((conv_pair_rs16<PD, 3, 1>), grid, block, pp.lds, s, x, y, a);
+    return hipGetLastError();
+}
+
 static hipError_t launch_pair(const PairPlan& pp, const PairArgs& a, const float* x, float* y, bool res,
                               hipStream_t s) {
+    if (a.mw == 3) {  // RS: the role-split stage-1 pair (no residual; checked by the caller)
+        if (res || pp.C != 16 || pp.waves != 7) return hipErrorInvalidValue;
+        return pp.pd == 3 ? launch_pair_rs<3>(pp, a, x, y, s) : hipErrorInvalidValue;
+    }
 #ifdef PO2Q_PAIR_DIAG
     if (const char* dv = getenv("PO2Q_PAIR_DEBUG")) {
         const int dbg = atoi(dv);
@@ -987,6 +1349,28 @@ int po2q_qconv2d_pair_f32(const float* x, const float* w1, const float* w2, floa
     // ring depths 3, 4 and 6 for the plain pair no different (r04_pair_mw_ab.jsonl): those variants are
     // gone.  PO2Q_PAIR_MW=0 selects the one-role kernel (A/B and test knob).
     a.mw = 0;
+    // The role-split stage-1 pair (conv_pair_rs16, 3 x-ring slots) for the forms without a residual at
+    // seven strips: 0.392 vs 0.414 ms for the memory-wave kernel, bench 25.83k vs 25.43k img/s
+    // (profiles/r06_pair16_rs_ab.jsonl; ring depths 2 / 4: 0.392 / 0.398).  PO2Q_PAIR_RS=0 turns it off;
+    // an explicit PO2Q_PAIR_MW or PO2Q_PAIR_VARIANT selects the kernels those knobs name (A/B and tests).
+    {
+        const char* rsv = getenv("PO2Q_PAIR_RS");
+        const bool rs_on = rsv ? rsv[0] != '0' : (!getenv("PO2Q_PAIR_MW") && !getenv("PO2Q_PAIR_VARIANT"));
+        const int d = 3;
+        if (rs_on && C == 16 && W > 6 * 32 && !residual) {
+            a.mw = 3;
+            if (!po2q::pair_plan(pp, (int)N, (int)C, (int)H, (int)W, false, d, 3)) {
+                po2q::set_error("po2q: pair: no role-split plan for this shape");
+                return PO2Q_ERR_UNSUPPORTED;
+            }
+            const hipError_t e = po2q::launch_pair(pp, a, x, y, false, reinterpret_cast<hipStream_t>(stream));
+            if (e != hipSuccess) {
+                po2q::set_error(std::string("po2q: pair launch: ") + hipGetErrorString(e));
+                return PO2Q_ERR_HIP;
+            }
+            return PO2Q_OK;
+        }
+    }
     const char* mv = getenv("PO2Q_PAIR_MW");
     if (!mv && C == 16 && !getenv("PO2Q_PAIR_VARIANT")) mv = "5";
     if (mv) {

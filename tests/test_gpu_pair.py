@@ -211,9 +211,34 @@ def test_pair_memory_wave_bitwise_equal(pd, shape, monkeypatch):
         outs.append(y)
     t = torch_chain(x, w1, w2, e, "relu", "relu6", None)  # forms[1]
     assert nerr(outs[1], t) <= CONV_TOL
-    if C == 16 and W > 192 and pd == 5:  # 7-wave widths: with PO2Q_PAIR_MW unset the default is MW at PD 5
-        monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)
+    if C == 16 and W > 192 and pd == 5:  # 7-wave widths: with PO2Q_PAIR_MW unset the default is the
+        monkeypatch.delenv("PO2Q_PAIR_MW", raising=False)  # role-split kernel without a residual, MW with one
         assert torch.equal(_lib.qconv2d_pair(x, w1, w2, 4, "po2"), outs[0])
+        assert torch.equal(_lib.qconv2d_pair(x, w1, w2, 4, "po2", **forms[2]), outs[2])
+
+
+@pytest.mark.parametrize("shape", [(2, 23, 224), (1, 224, 224), (3, 9, 200), (2, 1, 208), (4, 40, 224),
+                                   (1, 2, 193)])
+def test_pair_role_split_bitwise_equal_memory_wave(shape, monkeypatch):
+    """Stage 1's role-split pair (conv_pair_rs16: seven conv-1 waves DMA and split x and write the
+    intermediate ring, seven conv-2 waves read it two rows behind; the default at C = 16, W > 192
+    without a residual) runs the memory-wave kernel's fragments, MFMA order and epilogue expressions,
+    so its output is that kernel's bit for bit (PO2Q_PAIR_RS=0), plain and with the general epilogue;
+    ragged heights, 1- and 2-row images and the narrowest 7-strip width included."""
+    N, H, W = shape
+    x, w1, w2, e = make(N, H, W, 61 + H + W, True, 16)
+    g = torch.Generator().manual_seed(H * W)
+    b1, b2 = (torch.randn(16, generator=g) * 0.1).to(DEV), (torch.randn(16, generator=g) * 0.1).to(DEV)
+    forms = [{}, dict(act1="relu", act2="relu6", **e), dict(act1="silu", act2="relu", bias1=b1, bias2=b2, **e)]
+    for mode in ("po2", "po2+"):
+        for kw in forms:
+            monkeypatch.setenv("PO2Q_PAIR_RS", "0")
+            ref = _lib.qconv2d_pair(x, w1, w2, 4, mode, **kw)
+            monkeypatch.delenv("PO2Q_PAIR_RS")
+            y = _lib.qconv2d_pair(x, w1, w2, 4, mode, **kw)
+            assert torch.equal(y, ref), (shape, mode, sorted(kw), nerr(y, ref))
+    t = torch_chain(x, w1, w2, e, "relu", "relu6", None)
+    assert nerr(_lib.qconv2d_pair(x, w1, w2, 4, "po2", **forms[1]), t) <= CONV_TOL
 
 
 @pytest.mark.parametrize("shape", [(2, 23, 112, 32), (1, 112, 112, 32), (3, 9, 100, 32), (2, 1, 104, 32),
