@@ -15,7 +15,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--per-step", type=int, default=9, help="calls of --first per step")
-    ap.add_argument("--first", default="conv_pair<16", help="a kernel called --per-step times per step")
+    ap.add_argument("--first", default="conv_pair_rs16<", help="a kernel called --per-step times per step")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
