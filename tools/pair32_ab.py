@@ -2,7 +2,7 @@
 each arm is a set of env settings applied around its calls (the C ABI reads them per call), the arms are
 timed in interleaved rounds (HIP events, 11 launches each), medians printed as JSON lines.
   PAIR_AB_ARMS="PO2Q_PAIR_W32=0;PO2Q_PAIR_W32=2;PO2Q_PAIR_W32=3"  (';' between arms, ',' between vars)
-  PAIR_AB_FORM=plain|block   (block: BN affine + ReLU, the identity residual -- BasicBlock.forward)"""
+  PAIR_AB_FORM=plain|block|general   (general: BN affine + activations, no residual; block: BN affine + ReLU, the identity residual -- BasicBlock.forward)"""
 import json
 import os
 import sys
@@ -29,6 +29,10 @@ def main():
         kw = dict(post_scale1=torch.rand(C, device=dev) + 0.5, post_shift1=torch.randn(C, device=dev) * 0.1,
                   post_scale2=torch.rand(C, device=dev) + 0.5, post_shift2=torch.randn(C, device=dev) * 0.1,
                   act1="relu", act2="relu", residual=x)
+    elif form == "general":  # BN affine + activations, no residual
+        kw = dict(post_scale1=torch.rand(C, device=dev) + 0.5, post_shift1=torch.randn(C, device=dev) * 0.1,
+                  post_scale2=torch.rand(C, device=dev) + 0.5, post_shift2=torch.randn(C, device=dev) * 0.1,
+                  act1="relu", act2="relu6")
     nbytes = 4.0 * (2 * N * C * H * H + 4 * C * C * 9)
     flops = 2 * 2.0 * N * C * H * H * C * 9
     res = {}
